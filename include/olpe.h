@@ -1,0 +1,151 @@
+/*
+ * olpe.h -- C-ABI of libolpe.so, the MI355X (gfx950) implementation of the
+ * apf_step2 Gibbs/Metropolis-Hastings hot path of logan-pearce/olpefit.
+ *
+ * The reference has no FFI: its seam is the call sequence at
+ * apf_step2.py:312-318 (build_analytical_model -> chi_squared -> accept_reject)
+ * driven by the loop at :300-365, module-level functions reading the globals
+ * xsize/ysize.  Each entry point below names the reference code it replaces.
+ *
+ * Conventions
+ *  - Every int-returning call returns OLPE_OK (0) or a negative OLPE_E* code and
+ *    never aborts; olpe_last_error() gives a thread-local message.
+ *  - The caller owns every host buffer.  A context owns the device copies of the
+ *    image / inverse-sigma map and of the walker ensemble (state, counters, RNG).
+ *  - One context is bound to one HIP device (no CPU path: device < 0 or a host
+ *    without a GPU is an error).  Calls on one context are not thread-safe;
+ *    separate contexts (one per GPU) may be used concurrently.
+ *  - Parameter vectors use the reference layout: P = 16 (nsrc 2,
+ *    apf_step2.py:108) or 19 (nsrc 3, 3body/apf_step2_3body.py:266-288)
+ *    proposable parameters followed by the chi^2 slot, PS = P + 1 doubles.
+ */
+#ifndef OLPE_H
+#define OLPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OLPE_OK 0
+#define OLPE_EINVAL (-1)  /* bad argument */
+#define OLPE_EHIP (-2)    /* HIP runtime error / no GPU */
+#define OLPE_ENOMEM (-3)  /* device allocation failed */
+#define OLPE_ESTATE (-4)  /* call out of order (e.g. run before seeding) */
+#define OLPE_ECOMM (-5)   /* RCCL error */
+
+#define OLPE_DTYPE_F32 0
+#define OLPE_DTYPE_F64 1
+
+#define OLPE_EVAL_EXACT 0 /* one exp per pixel-Gaussian, reference op order */
+#define OLPE_EVAL_FAST 1  /* separable/recurrence evaluation */
+
+typedef struct olpe_ctx olpe_ctx;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int olpe_version(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int olpe_device_count(int *count);
+/* Thread-local message describing the last error. */
+const char *olpe_last_error(void);
+
+/* Create a context for one N x N cutout.  Replaces the setup at apf_step2.py:160-237:
+ *   image      ny*nx row-major, float32 (image_dtype OLPE_DTYPE_F32, BITPIX -32) or
+ *              float64; promoted to f64 exactly as ``data - model`` does (:135).
+ *   pois2      |D| Poisson term squared, same dtype as image, rounded as the
+ *              reference rounds it (``np.sqrt(np.abs(image))**2``, :207-210).
+ *   readnoise2 readnoise**2 (f64), :197-204.  err = sqrt(readnoise2 + pois2) (:210).
+ *   mask       u8, 1 = excluded (``np.ma.masked_greater(image, 0.8*satlevel)``, :188);
+ *              may be NULL (nothing masked).
+ *   ny == nx   the reference is square-only (:237 swaps the axes and :123 fails to
+ *              broadcast otherwise); ny != nx is OLPE_EINVAL.
+ *   nsrc       2 (apf_step2.py) or 3 (3body/apf_step2_3body.py).
+ *   bkgd_mode  0 = reference quirk, background fill p[12] (apf_step2.py:119-120);
+ *              1 = fill p[9] (the dead code at :126-132).  Ignored for nsrc 3.
+ *   device     HIP ordinal (>= 0). */
+int olpe_create(const void *image, int image_dtype, const void *pois2, double readnoise2,
+                const uint8_t *mask, int ny, int nx, int nsrc, int bkgd_mode, int device,
+                olpe_ctx **out);
+void olpe_destroy(olpe_ctx *ctx);
+/* Select OLPE_EVAL_EXACT (default) or OLPE_EVAL_FAST for the sampler. */
+int olpe_set_eval_mode(olpe_ctx *ctx, int mode);
+
+/* build_analytical_model (apf_step2.py:106-124; 3body :106-125): one PS-vector ->
+ * N*N f64 model image.  Test hook. */
+int olpe_model(olpe_ctx *ctx, const double *params, double *model_out);
+/* chi_squared(image_nanmask, build_analytical_model(p), err) (apf_step2.py:314-316,
+ * :134-137) for W parameter vectors [W][PS] -> chi2_out[W]. */
+int olpe_chi2_batch(olpe_ctx *ctx, const double *params, int W, double *chi2_out);
+
+/* --- walker ensemble (device resident) ------------------------------------------ */
+/* np.random.seed(seeds[w]) for W walkers (init_genrand semantics)
+ * and allocate the ensemble.  The reference seeds nothing (OS entropy per rank); the
+ * build seeds per walker so runs are reproducible and GPU-count independent. */
+int olpe_seed(olpe_ctx *ctx, const uint32_t *seeds, int W);
+/* Upload walker state [W][PS] (params + chi^2) and counters tries/accepts [W][P]
+ * (apf_step2.py:273-289; counters as the reference's float arrays, :276).
+ * tries/accepts may be NULL (zeros).  If chi^2 slots are NaN they are NOT recomputed:
+ * call olpe_chi2_batch first, as :283-289 does. */
+int olpe_state_set(olpe_ctx *ctx, const double *state, const double *tries,
+                   const double *accepts);
+int olpe_state_get(olpe_ctx *ctx, double *state, double *tries, double *accepts);
+/* Run n_iters Gibbs iterations of every walker (the loop body apf_step2.py:300-333)
+ * asynchronously on the context's stream.  The ensemble keeps a global iteration
+ * count c; the state after iteration c is recorded when c >= burn_in and
+ * (c - burn_in) % record_stride == 0 (apf_step2.py:342-351 with stride 1) into the
+ * device chain buffer of this launch (read with olpe_chain_read).  record_stride 0
+ * records nothing.  accept_min > 0 tracks, per walker, the first c at which every
+ * parameter has been tried accept_min times (the loop condition :300); read it with
+ * olpe_done_at.  *nrec_out (may be NULL) = rows recorded per walker by this launch. */
+int olpe_run(olpe_ctx *ctx, long long n_iters, long long burn_in, int record_stride,
+             long long accept_min, long long *nrec_out);
+/* Copy the last launch's chain [W][nrec][PS] to the host (synchronises). */
+int olpe_chain_read(olpe_ctx *ctx, double *chain_out);
+/* Iteration count of the ensemble (iterations completed so far). */
+int olpe_count(olpe_ctx *ctx, long long *count);
+int olpe_count_reset(olpe_ctx *ctx, long long count);
+/* Per walker: first count c with min(tries) >= accept_min, or -1. */
+int olpe_done_at(olpe_ctx *ctx, long long *done_at);
+/* One-shot form of the loop: upload state/tries/accepts for W
+ * walkers (already seeded with olpe_seed), reset the count to 0, run, download.
+ * chain_out [W][nrec][PS] may be NULL. */
+int olpe_run_gibbs(olpe_ctx *ctx, double *state, double *tries, double *accepts, int W,
+                   long long n_iters, long long burn_in, int record_stride,
+                   double *chain_out);
+
+/* RNG state for resume/parity: mt_state [W][625] = 624 key words + position,
+ * gauss_cache [W][2] = {has_gauss, cached deviate}. */
+int olpe_rng_get(olpe_ctx *ctx, uint32_t *mt_state, double *gauss_cache);
+int olpe_rng_set(olpe_ctx *ctx, const uint32_t *mt_state, const double *gauss_cache);
+/* Test hook: draw n values per walker from the ensemble streams.
+ * kind 0 = raw u32 (out as uint32 [W][n]); 1 = rand() f64; 2 = gauss f64;
+ * 3 = randint(0, P) as f64.  Advances the streams. */
+int olpe_rng_stream(olpe_ctx *ctx, int kind, int n, void *out);
+
+/* Per-iteration trace of the next olpe_run (test hook): on != 0 enables it.
+ * olpe_trace_read: [W][n_iters][6] f64 = {r, proposed value, chi^2 proposal, dice,
+ * p_accept, accepted}. */
+int olpe_trace_enable(olpe_ctx *ctx, int on);
+int olpe_trace_read(olpe_ctx *ctx, double *out);
+
+/* Wait for the context's stream. */
+int olpe_sync(olpe_ctx *ctx);
+/* Duration (ms, HIP events on the launch stream) of the last sampler launch. */
+int olpe_last_kernel_ms(olpe_ctx *ctx, double *ms);
+
+/* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
+/* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
+int olpe_comm_unique_id(uint8_t *id128);
+int olpe_comm_init(olpe_ctx *ctx, const uint8_t *id128, int nranks, int rank);
+/* All-gather the walker states of every rank: out [nranks*W][PS] (rank-major). */
+int olpe_comm_allgather_state(olpe_ctx *ctx, double *out);
+/* All-reduce per-parameter moments of the last launch's chain (or of the final
+ * states when no chain was recorded): out[3*PS] = {n, sum[PS], sumsq[PS]} with n
+ * repeated in slot 0 of the first block, see DESIGN.md §6. */
+int olpe_comm_allreduce_moments(olpe_ctx *ctx, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OLPE_H */

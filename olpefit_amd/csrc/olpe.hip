@@ -1,0 +1,900 @@
+// olpe.hip -- gfx950 kernels and the C-ABI (include/olpe.h) of libolpe.so.
+//
+// Kernels
+//   olpe_gibbs_kernel  fused sampler: W walkers, one per wavefront, n_iters Gibbs
+//                      iterations each (apf_step2.py:300-351) with the cutout and
+//                      inverse-sigma map staged once per workgroup into LDS.
+//   olpe_model_kernel  build_analytical_model for one vector (test hook)
+//   olpe_chi2_kernel   chi_squared for a batch of vectors (the minimum slice)
+//   olpe_seed_kernel   np.random.seed per walker
+//   olpe_stream_kernel RNG stream dump (test hook)
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/olpe.h"
+#include "olpe_device.h"
+#include "olpe_internal.h"
+
+using namespace olpe;
+
+namespace {
+
+// ---------------------------------------------------------------------------------
+// Jump widths (apf_step2.py:234; 3body/apf_step2_3body.py:220-238)
+// ---------------------------------------------------------------------------------
+__constant__ double c_widths2[16] = {0.01, 0.01, 0.3,   0.3,    0.08,  0.09,
+                                     0.0025, 0.02, 0.001, 0.0008, 0.002, 0.002,
+                                     0.001, 0.001, 0.008, 0.01};
+__constant__ double c_widths3[19] = {0.01,  0.01,  0.3,   0.3,  0.3,   0.3,   0.08,
+                                     0.09,  0.0025, 0.02, 0.02, 0.001, 0.0008, 0.002,
+                                     0.002, 0.001, 0.001, 0.008, 0.01};
+
+template <int NSRC> __device__ __forceinline__ double width_of(int r) {
+  return NSRC == 2 ? c_widths2[r] : c_widths3[r];
+}
+
+struct GibbsArgs {
+  const double *D;     // [n*n] f64 data (0 where masked)
+  const double *invE;  // [n*n] 1/err (0 where masked)
+  int n;
+  int bkgd_mode;
+  long long W;
+  double *state;       // [W][PS]
+  uint32_t *tries;     // [W][NP]
+  uint32_t *accepts;   // [W][NP]
+  uint32_t *mt;        // [W][624]
+  int *mt_pos;         // [W]
+  double *gauss;       // [W]
+  int *has_gauss;      // [W]
+  long long *done_at;  // [W]
+  long long n_iters;
+  long long count0;
+  long long burn_in;
+  long long stride;    // 0 = no chain
+  long long row0;      // global row index of the first row of this launch
+  long long nrows;     // rows per walker in `chain`
+  double *chain;       // [W][nrows][PS]
+  long long accept_min;
+  double *trace;       // [W][n_iters][6] or null
+};
+
+constexpr int kTraceF = 6;
+
+// ---------------------------------------------------------------------------------
+// The fused sampler
+// ---------------------------------------------------------------------------------
+// Per-wave LDS slice: MT key[624] | tries[NP] | accepts[NP] | state doubles (below)
+template <int NP> struct WaveSlice {
+  static constexpr int U32 = MT_N + 2 * NP;                  // 8-byte multiple for NP 16/19
+  static constexpr int PS = NP + 1;
+  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
+  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
+  static constexpr int OPT = PS + 12, OPC = PS + 15;
+  static constexpr int F64 = PS + 18;
+  static constexpr int BYTES = U32 * 4 + F64 * 8;
+};
+static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
+
+__device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
+__device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }
+__device__ __forceinline__ void st_trig(double *s, const Trig &t) {
+  s[0] = t.cost2; s[1] = t.sint2; s[2] = t.sin2t;
+}
+__device__ __forceinline__ void st_coef(double *s, const Coef &k) {
+  s[0] = k.a; s[1] = k.b; s[2] = k.c;
+}
+
+template <int NSRC, int NT, bool LDS_IMG, int WPB>
+__global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
+  using L = Layout<NSRC>;
+  using WS = WaveSlice<L::NP>;
+  constexpr int NP = L::NP, PS = L::PS;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = NT ? NT : A.n;
+  const int npix = n * n;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+
+  // ---- LDS carve: [D | invE] (if staged) then one WaveSlice per wave
+  const int npad = (npix + 1) & ~1;   // keep sE 16-byte aligned
+  double *sD = reinterpret_cast<double *>(smem);
+  double *sE = sD + (LDS_IMG ? npad : 0);
+  unsigned char *wb = reinterpret_cast<unsigned char *>(sE + (LDS_IMG ? npad : 0)) +
+                      (size_t)wave * WS::BYTES;
+  uint32_t *key = reinterpret_cast<uint32_t *>(wb);
+  uint32_t *s_tries = key + MT_N;
+  uint32_t *s_acc = s_tries + NP;
+  double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
+
+  if constexpr (LDS_IMG) {
+    // one coalesced 16-B-per-lane staging pass of the cutout and 1/err
+    const int nv = npix / 2;
+    const double2 *gD = reinterpret_cast<const double2 *>(A.D);
+    const double2 *gE = reinterpret_cast<const double2 *>(A.invE);
+    double2 *lD = reinterpret_cast<double2 *>(sD);
+    double2 *lE = reinterpret_cast<double2 *>(sE);
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) {
+      lD[k] = gD[k];
+      lE[k] = gE[k];
+    }
+    if ((npix & 1) && threadIdx.x == 0) {
+      sD[npix - 1] = A.D[npix - 1];
+      sE[npix - 1] = A.invE[npix - 1];
+    }
+    __syncthreads();
+  }
+  const double *D = LDS_IMG ? sD : A.D;
+  const double *invE = LDS_IMG ? sE : A.invE;
+
+  const long long w = (long long)blockIdx.x * WPB + wave;
+  if (w >= A.W) return;
+
+  // ---- walker state -> LDS slice
+  for (int k = lane; k < MT_N; k += 64) key[k] = A.mt[w * MT_N + k];
+  if (lane < NP) {
+    s_tries[lane] = A.tries[w * NP + lane];
+    s_acc[lane] = A.accepts[w * NP + lane];
+  }
+  if (lane < PS) st[lane] = A.state[w * PS + lane];
+  wave_sync();
+  if (lane == 0) {
+    const Trig t1 = make_trig(st[L::T1]), t2 = make_trig(st[L::T2]);
+    st_trig(st + WS::OT1, t1);
+    st_trig(st + WS::OT2, t2);
+    st_coef(st + WS::OC1, make_coef(st[L::S1X], st[L::S1Y], t1));
+    st_coef(st + WS::OC2, make_coef(st[L::S2X], st[L::S2Y], t2));
+  }
+  wave_sync();
+
+  MTWave mt;
+  mt.key = key;
+  mt.pos = __builtin_amdgcn_readfirstlane(A.mt_pos[w]);
+  mt.bstart = mt.pos;
+  mt.bsize = 0;
+  mt.batch = 0;
+  mt.has_gauss = __builtin_amdgcn_readfirstlane(A.has_gauss[w]);
+  mt.gauss = uniform_f64(A.gauss[w]);
+
+  int ndone = 0;
+  long long done_at = A.done_at[w];
+  if (A.accept_min > 0) {
+    for (int k = 0; k < NP; ++k) ndone += (s_tries[k] >= (uint32_t)A.accept_min);
+    ndone = __builtin_amdgcn_readfirstlane(ndone);
+  }
+
+  long long count = A.count0;
+  for (long long it = 0; it < A.n_iters; ++it) {
+    // randint(0, NP)  (apf_step2.py:302)
+    const int r = __builtin_amdgcn_readfirstlane(mt.template randint<NP>(lane));
+    // total_tries[rand] += 1  (:304)
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
+    wave_sync();
+    if (lane == 0) s_tries[r] = tr;
+    if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) ++ndone;
+
+    // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
+    const double cur = uniform_f64(st[r]);
+    const double g = mt.gauss_next(lane);
+    const double wr = width_of<NSRC>(r);
+    double nv;
+    if ((L::LOGMASK >> r) & 1u) {
+      const double lv = log10(cur);
+      nv = pow(10.0, lv + wr * g);
+    } else {
+      nv = cur + wr * g;
+    }
+    nv = uniform_f64(nv);
+
+    // coefficient sets of the proposal: only the set that r touches is rebuilt
+    auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
+    const int grp = (r == L::S1X || r == L::S1Y || r == L::T1) ? 1
+                  : (r == L::S2X || r == L::S2Y || r == L::T2) ? 2 : 0;
+    Coef C1p, C2p;
+    if (grp == 1) {
+      const Trig t = (r == L::T1) ? make_trig(nv) : ld_trig(st + WS::OT1);
+      C1p = make_coef(q(L::S1X), q(L::S1Y), t);
+      if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
+    } else {
+      C1p = ld_coef(st + WS::OC1);
+    }
+    if (grp == 2) {
+      const Trig t = (r == L::T2) ? make_trig(nv) : ld_trig(st + WS::OT2);
+      C2p = make_coef(q(L::S2X), q(L::S2Y), t);
+      if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
+    } else {
+      C2p = ld_coef(st + WS::OC2);
+    }
+    const ModelDesc<NSRC> md = make_model<NSRC>(q, C1p, C2p, A.bkgd_mode);
+
+    // build_analytical_model + chi_squared (:314-316)
+    const double part = sweep_exact<NSRC, NT, false>(md, D, invE, nullptr, n, lane);
+    const double chi = wave_sum(part);
+
+    // accept_reject (:139-148)
+    const double p_accept = exp(-(chi - st[PS - 1]) / 2.);
+    const double dice = mt.rand53(lane);
+    const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
+    wave_sync();
+    if (acc && lane == 0) {
+      s_acc[r] = s_acc[r] + 1u;
+      st[r] = nv;
+      st[PS - 1] = chi;
+      if (grp) {
+        double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
+        double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
+        for (int k = 0; k < 3; ++k) { dt[k] = st[WS::OPT + k]; dc[k] = st[WS::OPC + k]; }
+      }
+    }
+    wave_sync();
+    ++count;
+    if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = count;
+
+    if (A.trace && lane == 0) {
+      double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
+      t[0] = (double)r;
+      t[1] = nv;
+      t[2] = chi;
+      t[3] = dice;
+      t[4] = p_accept;
+      t[5] = acc ? 1.0 : 0.0;
+    }
+    // chain record (:342-351, generalised to a stride)
+    if (A.stride > 0 && count >= A.burn_in && (count - A.burn_in) % A.stride == 0) {
+      const long long row = (count - A.burn_in) / A.stride - A.row0;
+      if (row >= 0 && row < A.nrows && lane < PS)
+        A.chain[((size_t)w * A.nrows + row) * PS + lane] = st[lane];
+    }
+  }
+
+  // ---- write back
+  wave_sync();
+  if (lane < PS) A.state[w * PS + lane] = st[lane];
+  if (lane < NP) {
+    A.tries[w * NP + lane] = s_tries[lane];
+    A.accepts[w * NP + lane] = s_acc[lane];
+  }
+  for (int k = lane; k < MT_N; k += 64) A.mt[w * MT_N + k] = key[k];
+  if (lane == 0) {
+    A.mt_pos[w] = mt.pos;
+    A.has_gauss[w] = mt.has_gauss;
+    A.gauss[w] = mt.gauss;
+    A.done_at[w] = done_at;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Model / chi^2 of explicit parameter vectors (one wave per vector; image in global)
+// ---------------------------------------------------------------------------------
+template <int NSRC, bool WRITE>
+__global__ __launch_bounds__(256) void olpe_eval_kernel(const double *D, const double *invE,
+                                                        int n, int bkgd_mode,
+                                                        const double *params, int W,
+                                                        double *out) {
+  using L = Layout<NSRC>;
+  constexpr int PS = L::PS;
+  const int lane = threadIdx.x & 63;
+  const long long w = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (w >= W) return;
+  double p[PS];
+#pragma unroll
+  for (int k = 0; k < PS; ++k) p[k] = uniform_f64(params[w * PS + k]);
+  const Trig T1 = make_trig(p[L::T1]), T2 = make_trig(p[L::T2]);
+  const Coef C1 = make_coef(p[L::S1X], p[L::S1Y], T1);
+  const Coef C2 = make_coef(p[L::S2X], p[L::S2Y], T2);
+  auto q = [&](int k) -> double { return p[k]; };
+  const ModelDesc<NSRC> md = make_model<NSRC>(q, C1, C2, bkgd_mode);
+  if constexpr (WRITE) {
+    sweep_exact<NSRC, 0, true>(md, D, invE, out + (size_t)w * n * n, n, lane);
+  } else {
+    const double chi = wave_sum(sweep_exact<NSRC, 0, false>(md, D, invE, nullptr, n, lane));
+    if (lane == 0) out[w] = chi;
+  }
+}
+
+__global__ void olpe_seed_kernel(const uint32_t *seeds, int W, uint32_t *mt, int *pos,
+                                 int *has_gauss, double *gauss) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  mt_seed_serial(mt + (size_t)w * MT_N, seeds[w]);
+  pos[w] = MT_N;
+  has_gauss[w] = 0;
+  gauss[w] = 0.0;
+}
+
+// RNG stream dump: one wave per walker, same draw path as the sampler.
+template <int NP>
+__global__ __launch_bounds__(64) void olpe_stream_kernel(uint32_t *mtg, int *posg,
+                                                         int *hasg, double *gg, int W,
+                                                         int kind, int nd, void *out) {
+  __shared__ uint32_t key[MT_N];
+  const int lane = threadIdx.x;
+  const int w = blockIdx.x;
+  if (w >= W) return;
+  for (int k = lane; k < MT_N; k += 64) key[k] = mtg[(size_t)w * MT_N + k];
+  wave_sync();
+  MTWave mt;
+  mt.key = key;
+  mt.pos = __builtin_amdgcn_readfirstlane(posg[w]);
+  mt.bstart = mt.pos;
+  mt.bsize = 0;
+  mt.batch = 0;
+  mt.has_gauss = __builtin_amdgcn_readfirstlane(hasg[w]);
+  mt.gauss = uniform_f64(gg[w]);
+  for (int i = 0; i < nd; ++i) {
+    if (kind == 0) {
+      const uint32_t v = mt.next(lane);
+      if (lane == 0) reinterpret_cast<uint32_t *>(out)[(size_t)w * nd + i] = v;
+    } else {
+      double v;
+      if (kind == 1) v = mt.rand53(lane);
+      else if (kind == 2) v = mt.gauss_next(lane);
+      else v = (double)mt.template randint<NP>(lane);
+      if (lane == 0) reinterpret_cast<double *>(out)[(size_t)w * nd + i] = v;
+    }
+  }
+  wave_sync();
+  for (int k = lane; k < MT_N; k += 64) mtg[(size_t)w * MT_N + k] = key[k];
+  if (lane == 0) {
+    posg[w] = mt.pos;
+    hasg[w] = mt.has_gauss;
+    gg[w] = mt.gauss;
+  }
+}
+
+}  // namespace
+
+// =================================================================================
+// Host side
+// =================================================================================
+namespace olpe {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+}  // namespace olpe
+
+#define HIPCHK(expr)                                                                \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      return set_err(OLPE_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));     \
+  } while (0)
+
+namespace {
+
+template <class T> int dev_alloc(T **p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) return OLPE_OK;
+  hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T),
+                   hipGetErrorString(e));
+  }
+  return OLPE_OK;
+}
+
+size_t lds_bytes(const olpe_ctx *c, int wpb) {
+  size_t b = (size_t)wpb * (c->np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES);
+  if (c->lds_img) b += (size_t)((c->n * c->n + 1) & ~1) * 2 * sizeof(double);
+  return b;
+}
+
+template <int NSRC, int NT, bool LDS, int WPB>
+int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
+  const size_t shm = lds_bytes(c, WPB);
+  auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIPCHK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024));
+    attr_set = true;
+  }
+  const unsigned blocks = (unsigned)((a.W + WPB - 1) / WPB);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, a);
+  HIPCHK(hipGetLastError());
+  return OLPE_OK;
+}
+
+template <int NSRC> int launch_gibbs_n(olpe_ctx *c, const GibbsArgs &a) {
+  if (c->lds_img) {
+    switch (c->n) {
+      case 32: return launch_gibbs_t<NSRC, 32, true, 16>(c, a);
+      case 64: return launch_gibbs_t<NSRC, 64, true, 16>(c, a);
+      default: return launch_gibbs_t<NSRC, 0, true, 16>(c, a);
+    }
+  }
+  if (c->n == 128) return launch_gibbs_t<NSRC, 128, false, 4>(c, a);
+  return launch_gibbs_t<NSRC, 0, false, 4>(c, a);
+}
+
+int launch_gibbs(olpe_ctx *c, const GibbsArgs &a) {
+  return c->nsrc == 2 ? launch_gibbs_n<2>(c, a) : launch_gibbs_n<3>(c, a);
+}
+
+int ensure_ensemble(olpe_ctx *c, int W) {
+  if (W <= 0) return set_err(OLPE_EINVAL, "W must be > 0 (got %d)", W);
+  if (c->W == W && c->d_state) return OLPE_OK;
+  int rc;
+  if ((rc = dev_alloc(&c->d_state, (size_t)W * c->ps))) return rc;
+  if ((rc = dev_alloc(&c->d_tries, (size_t)W * c->np))) return rc;
+  if ((rc = dev_alloc(&c->d_acc, (size_t)W * c->np))) return rc;
+  if ((rc = dev_alloc(&c->d_mt, (size_t)W * MT_N))) return rc;
+  if ((rc = dev_alloc(&c->d_mtpos, (size_t)W))) return rc;
+  if ((rc = dev_alloc(&c->d_gauss, (size_t)W))) return rc;
+  if ((rc = dev_alloc(&c->d_hasg, (size_t)W))) return rc;
+  if ((rc = dev_alloc(&c->d_done, (size_t)W))) return rc;
+  HIPCHK(hipMemsetAsync(c->d_state, 0, (size_t)W * c->ps * sizeof(double), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_tries, 0, (size_t)W * c->np * sizeof(uint32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_acc, 0, (size_t)W * c->np * sizeof(uint32_t), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_done, 0xff, (size_t)W * sizeof(long long), c->stream));
+  c->W = W;
+  c->seeded = false;
+  c->count = 0;
+  c->chain_rows = 0;
+  return OLPE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int olpe_version(void) { return 100; }
+
+const char *olpe_last_error(void) { return g_err; }
+
+int olpe_device_count(int *count) {
+  if (!count) return set_err(OLPE_EINVAL, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = (e == hipSuccess) ? n : 0;
+  return OLPE_OK;
+}
+
+int olpe_create(const void *image, int image_dtype, const void *pois2, double readnoise2,
+                const uint8_t *mask, int ny, int nx, int nsrc, int bkgd_mode, int device,
+                olpe_ctx **out) {
+  if (!out) return set_err(OLPE_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!image || !pois2) return set_err(OLPE_EINVAL, "image/pois2 is NULL");
+  if (ny <= 0 || nx <= 0) return set_err(OLPE_EINVAL, "bad shape %dx%d", ny, nx);
+  if (ny != nx)
+    return set_err(OLPE_EINVAL,
+                   "non-square image %dx%d: the reference model is square-only "
+                   "(apf_step2.py:237, :119-123)", ny, nx);
+  if (nx > 4096) return set_err(OLPE_EINVAL, "image too large (%d)", nx);
+  if (nsrc != 2 && nsrc != 3) return set_err(OLPE_EINVAL, "nsrc must be 2 or 3");
+  if (image_dtype != OLPE_DTYPE_F32 && image_dtype != OLPE_DTYPE_F64)
+    return set_err(OLPE_EINVAL, "image_dtype must be OLPE_DTYPE_F32/F64");
+  if (bkgd_mode != 0 && bkgd_mode != 1) return set_err(OLPE_EINVAL, "bkgd_mode must be 0/1");
+  if (device < 0) return set_err(OLPE_EINVAL, "device must be a HIP ordinal (no CPU path)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return set_err(OLPE_EHIP, "no HIP device visible");
+  if (device >= ndev) return set_err(OLPE_EINVAL, "device %d >= device count %d", device, ndev);
+  HIPCHK(hipSetDevice(device));
+
+  olpe_ctx *c = new olpe_ctx();
+  c->device = device;
+  c->n = nx;
+  c->nsrc = nsrc;
+  c->bkgd_mode = bkgd_mode;
+  c->np = nsrc == 2 ? 16 : 19;
+  c->ps = c->np + 1;
+  const size_t npix = (size_t)nx * nx;
+  // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
+  const size_t slice = c->np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES;
+  c->lds_img = (((npix + 1) & ~(size_t)1) * 16 + 16 * slice) <= 160 * 1024;
+
+  std::vector<double> hD(npix), hE(npix);
+  for (size_t i = 0; i < npix; ++i) {
+    const double d = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)image)[i]
+                                                   : ((const double *)image)[i];
+    const double p2 = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)pois2)[i]
+                                                    : ((const double *)pois2)[i];
+    const double e = sqrt(readnoise2 + p2);   // apf_step2.py:210
+    if (mask && mask[i]) {
+      hD[i] = 0.0;
+      hE[i] = 0.0;
+    } else {
+      hD[i] = d;
+      hE[i] = 1.0 / e;
+    }
+  }
+  int rc;
+  hipError_t e1 = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e1 != hipSuccess) {
+    delete c;
+    return set_err(OLPE_EHIP, "hipStreamCreate: %s", hipGetErrorString(e1));
+  }
+  (void)hipEventCreate(&c->ev0);
+  (void)hipEventCreate(&c->ev1);
+  if ((rc = dev_alloc(&c->d_D, npix)) || (rc = dev_alloc(&c->d_invE, npix))) {
+    olpe_destroy(c);
+    return rc;
+  }
+  hipError_t e2 = hipMemcpy(c->d_D, hD.data(), npix * 8, hipMemcpyHostToDevice);
+  hipError_t e3 = hipMemcpy(c->d_invE, hE.data(), npix * 8, hipMemcpyHostToDevice);
+  if (e2 != hipSuccess || e3 != hipSuccess) {
+    olpe_destroy(c);
+    return set_err(OLPE_EHIP, "hipMemcpy image: %s",
+                   hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+  }
+  *out = c;
+  return OLPE_OK;
+}
+
+void olpe_destroy(olpe_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  olpe_comm_release(c);
+  void *ptrs[] = {c->d_D,  c->d_invE,  c->d_state, c->d_tries, c->d_acc,
+                  c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
+                  c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int olpe_set_eval_mode(olpe_ctx *c, int mode) {
+  if (!c) return set_err(OLPE_EINVAL, "ctx is NULL");
+  if (mode != OLPE_EVAL_EXACT && mode != OLPE_EVAL_FAST)
+    return set_err(OLPE_EINVAL, "unknown eval mode %d", mode);
+  c->eval_mode = mode;
+  return OLPE_OK;
+}
+
+static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, bool write) {
+  if (!c || !params || !out) return set_err(OLPE_EINVAL, "NULL argument");
+  if (W <= 0) return set_err(OLPE_EINVAL, "W must be > 0");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t pin = (size_t)W * c->ps;
+  const size_t pout = write ? (size_t)W * c->n * c->n : (size_t)W;
+  int rc;
+  if (c->scratch_cap < pin && (rc = dev_alloc(&c->d_scratch, pin))) return rc;
+  if (c->scratch_cap < pin) c->scratch_cap = pin;
+  if (c->scratch2_cap < pout && (rc = dev_alloc(&c->d_scratch2, pout))) return rc;
+  if (c->scratch2_cap < pout) c->scratch2_cap = pout;
+  HIPCHK(hipMemcpyAsync(c->d_scratch, params, pin * 8, hipMemcpyHostToDevice, c->stream));
+  const int wpb = 4;
+  dim3 grid((W + wpb - 1) / wpb), block(wpb * 64);
+  if (c->nsrc == 2) {
+    if (write)
+      hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, 0, c->stream, c->d_D,
+                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+    else
+      hipLaunchKernelGGL((olpe_eval_kernel<2, false>), grid, block, 0, c->stream, c->d_D,
+                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+  } else {
+    if (write)
+      hipLaunchKernelGGL((olpe_eval_kernel<3, true>), grid, block, 0, c->stream, c->d_D,
+                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+    else
+      hipLaunchKernelGGL((olpe_eval_kernel<3, false>), grid, block, 0, c->stream, c->d_D,
+                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->d_scratch2, pout * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return OLPE_OK;
+}
+
+int olpe_model(olpe_ctx *c, const double *params, double *model_out) {
+  return eval_batch(c, params, 1, model_out, true);
+}
+
+int olpe_chi2_batch(olpe_ctx *c, const double *params, int W, double *chi2_out) {
+  return eval_batch(c, params, W, chi2_out, false);
+}
+
+int olpe_seed(olpe_ctx *c, const uint32_t *seeds, int W) {
+  if (!c || !seeds) return set_err(OLPE_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_ensemble(c, W))) return rc;
+  uint32_t *ds = nullptr;
+  if ((rc = dev_alloc(&ds, (size_t)W))) return rc;
+  HIPCHK(hipMemcpyAsync(ds, seeds, (size_t)W * 4, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(olpe_seed_kernel, dim3((W + 255) / 256), dim3(256), 0, c->stream, ds, W,
+                     c->d_mt, c->d_mtpos, c->d_hasg, c->d_gauss);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  (void)hipFree(ds);
+  c->seeded = true;
+  return OLPE_OK;
+}
+
+static int counters_to_dev(olpe_ctx *c, const double *h, uint32_t *d) {
+  const size_t m = (size_t)c->W * c->np;
+  std::vector<uint32_t> t(m, 0u);
+  if (h)
+    for (size_t i = 0; i < m; ++i) {
+      if (!(h[i] >= 0.0) || h[i] > 4294967295.0)
+        return set_err(OLPE_EINVAL, "counter %zu out of range (%g)", i, h[i]);
+      t[i] = (uint32_t)h[i];
+    }
+  HIPCHK(hipMemcpyAsync(d, t.data(), m * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return OLPE_OK;
+}
+
+static int counters_to_host(olpe_ctx *c, const uint32_t *d, double *h) {
+  const size_t m = (size_t)c->W * c->np;
+  std::vector<uint32_t> t(m);
+  HIPCHK(hipMemcpy(t.data(), d, m * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < m; ++i) h[i] = (double)t[i];
+  return OLPE_OK;
+}
+
+int olpe_state_set(olpe_ctx *c, const double *state, const double *tries,
+                   const double *accepts) {
+  if (!c || !state) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->d_state) return set_err(OLPE_ESTATE, "call olpe_seed first");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_state, state, (size_t)c->W * c->ps * 8, hipMemcpyHostToDevice,
+                        c->stream));
+  int rc;
+  if ((rc = counters_to_dev(c, tries, c->d_tries))) return rc;
+  if ((rc = counters_to_dev(c, accepts, c->d_acc))) return rc;
+  HIPCHK(hipMemsetAsync(c->d_done, 0xff, (size_t)c->W * sizeof(long long), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return OLPE_OK;
+}
+
+int olpe_state_get(olpe_ctx *c, double *state, double *tries, double *accepts) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (state)
+    HIPCHK(hipMemcpy(state, c->d_state, (size_t)c->W * c->ps * 8, hipMemcpyDeviceToHost));
+  int rc;
+  if (tries && (rc = counters_to_host(c, c->d_tries, tries))) return rc;
+  if (accepts && (rc = counters_to_host(c, c->d_acc, accepts))) return rc;
+  return OLPE_OK;
+}
+
+int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_stride,
+             long long accept_min, long long *nrec_out) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  if (!c->d_state || !c->seeded) return set_err(OLPE_ESTATE, "call olpe_seed first");
+  if (n_iters < 0 || burn_in < 0 || record_stride < 0 || accept_min < 0)
+    return set_err(OLPE_EINVAL, "negative argument");
+  HIPCHK(hipSetDevice(c->device));
+  // rows recorded in (count0, count0 + n_iters]
+  long long row0 = 0, nrows = 0;
+  const long long c0 = c->count, c1 = c->count + n_iters;
+  if (record_stride > 0 && c1 >= burn_in) {
+    const long long s = record_stride;
+    const long long lo = std::max(c0 + 1, burn_in);
+    const long long first = (lo - burn_in + s - 1) / s;   // first row index >= lo
+    const long long last = (c1 - burn_in) / s;            // last row index <= c1
+    if (last >= first) {
+      row0 = first;
+      nrows = last - first + 1;
+    }
+  }
+  int rc;
+  const size_t chain_need = (size_t)c->W * nrows * c->ps;
+  if (chain_need > c->chain_cap) {
+    if ((rc = dev_alloc(&c->d_chain, chain_need))) return rc;
+    c->chain_cap = chain_need;
+  }
+  c->chain_rows = nrows;
+  const size_t trace_need = c->trace_on ? (size_t)c->W * n_iters * kTraceF : 0;
+  if (trace_need > c->trace_cap) {
+    if ((rc = dev_alloc(&c->d_trace, trace_need))) return rc;
+    c->trace_cap = trace_need;
+  }
+  c->trace_iters = c->trace_on ? n_iters : 0;
+
+  GibbsArgs a;
+  a.D = c->d_D;
+  a.invE = c->d_invE;
+  a.n = c->n;
+  a.bkgd_mode = c->bkgd_mode;
+  a.W = c->W;
+  a.state = c->d_state;
+  a.tries = c->d_tries;
+  a.accepts = c->d_acc;
+  a.mt = c->d_mt;
+  a.mt_pos = c->d_mtpos;
+  a.gauss = c->d_gauss;
+  a.has_gauss = c->d_hasg;
+  a.done_at = c->d_done;
+  a.n_iters = n_iters;
+  a.count0 = c0;
+  a.burn_in = burn_in;
+  a.stride = nrows > 0 ? record_stride : 0;
+  a.row0 = row0;
+  a.nrows = nrows;
+  a.chain = c->d_chain;
+  a.accept_min = accept_min;
+  a.trace = c->trace_on ? c->d_trace : nullptr;
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if ((rc = launch_gibbs(c, a))) return rc;
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  c->count = c1;
+  if (nrec_out) *nrec_out = nrows;
+  return OLPE_OK;
+}
+
+int olpe_chain_read(olpe_ctx *c, double *chain_out) {
+  if (!c || !chain_out) return set_err(OLPE_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const size_t m = (size_t)c->W * c->chain_rows * c->ps;
+  if (m) HIPCHK(hipMemcpy(chain_out, c->d_chain, m * 8, hipMemcpyDeviceToHost));
+  return OLPE_OK;
+}
+
+int olpe_count(olpe_ctx *c, long long *count) {
+  if (!c || !count) return set_err(OLPE_EINVAL, "NULL argument");
+  *count = c->count;
+  return OLPE_OK;
+}
+
+int olpe_count_reset(olpe_ctx *c, long long count) {
+  if (!c || count < 0) return set_err(OLPE_EINVAL, "bad argument");
+  c->count = count;
+  return OLPE_OK;
+}
+
+int olpe_done_at(olpe_ctx *c, long long *done_at) {
+  if (!c || !done_at) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->d_done) return set_err(OLPE_ESTATE, "no ensemble");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(done_at, c->d_done, (size_t)c->W * 8, hipMemcpyDeviceToHost));
+  return OLPE_OK;
+}
+
+int olpe_run_gibbs(olpe_ctx *c, double *state, double *tries, double *accepts, int W,
+                   long long n_iters, long long burn_in, int record_stride,
+                   double *chain_out) {
+  if (!c || !state) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->seeded || c->W != W)
+    return set_err(OLPE_ESTATE, "seed %d walkers with olpe_seed first", W);
+  int rc;
+  if ((rc = olpe_state_set(c, state, tries, accepts))) return rc;
+  c->count = 0;
+  if ((rc = olpe_run(c, n_iters, burn_in, record_stride, 0, nullptr))) return rc;
+  if ((rc = olpe_state_get(c, state, tries, accepts))) return rc;
+  if (chain_out && (rc = olpe_chain_read(c, chain_out))) return rc;
+  return OLPE_OK;
+}
+
+int olpe_rng_get(olpe_ctx *c, uint32_t *mt_state, double *gauss_cache) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  if (!c->d_mt) return set_err(OLPE_ESTATE, "no ensemble");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int W = c->W;
+  if (mt_state) {
+    std::vector<uint32_t> key((size_t)W * MT_N);
+    std::vector<int> pos(W);
+    HIPCHK(hipMemcpy(key.data(), c->d_mt, key.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pos.data(), c->d_mtpos, (size_t)W * 4, hipMemcpyDeviceToHost));
+    for (int w = 0; w < W; ++w) {
+      memcpy(mt_state + (size_t)w * (MT_N + 1), key.data() + (size_t)w * MT_N, MT_N * 4);
+      mt_state[(size_t)w * (MT_N + 1) + MT_N] = (uint32_t)pos[w];
+    }
+  }
+  if (gauss_cache) {
+    std::vector<int> h(W);
+    std::vector<double> g(W);
+    HIPCHK(hipMemcpy(h.data(), c->d_hasg, (size_t)W * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(g.data(), c->d_gauss, (size_t)W * 8, hipMemcpyDeviceToHost));
+    for (int w = 0; w < W; ++w) {
+      gauss_cache[2 * w] = h[w];
+      gauss_cache[2 * w + 1] = g[w];
+    }
+  }
+  return OLPE_OK;
+}
+
+int olpe_rng_set(olpe_ctx *c, const uint32_t *mt_state, const double *gauss_cache) {
+  if (!c || !mt_state || !gauss_cache) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->d_mt) return set_err(OLPE_ESTATE, "no ensemble (call olpe_seed)");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int W = c->W;
+  std::vector<uint32_t> key((size_t)W * MT_N);
+  std::vector<int> pos(W), h(W);
+  std::vector<double> g(W);
+  for (int w = 0; w < W; ++w) {
+    memcpy(key.data() + (size_t)w * MT_N, mt_state + (size_t)w * (MT_N + 1), MT_N * 4);
+    pos[w] = (int)mt_state[(size_t)w * (MT_N + 1) + MT_N];
+    if (pos[w] < 0 || pos[w] > MT_N) return set_err(OLPE_EINVAL, "bad MT position");
+    h[w] = gauss_cache[2 * w] != 0.0;
+    g[w] = gauss_cache[2 * w + 1];
+  }
+  HIPCHK(hipMemcpy(c->d_mt, key.data(), key.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_mtpos, pos.data(), (size_t)W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_hasg, h.data(), (size_t)W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c->d_gauss, g.data(), (size_t)W * 8, hipMemcpyHostToDevice));
+  c->seeded = true;
+  return OLPE_OK;
+}
+
+int olpe_rng_stream(olpe_ctx *c, int kind, int n, void *out) {
+  if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
+  if (kind < 0 || kind > 3 || n <= 0) return set_err(OLPE_EINVAL, "bad kind/n");
+  if (!c->seeded) return set_err(OLPE_ESTATE, "call olpe_seed first");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t esz = kind == 0 ? 4 : 8;
+  const size_t bytes = (size_t)c->W * n * esz;
+  void *d = nullptr;
+  HIPCHK(hipMalloc(&d, bytes));
+  if (c->np == 16)
+    hipLaunchKernelGGL(olpe_stream_kernel<16>, dim3(c->W), dim3(64), 0, c->stream, c->d_mt,
+                       c->d_mtpos, c->d_hasg, c->d_gauss, c->W, kind, n, d);
+  else
+    hipLaunchKernelGGL(olpe_stream_kernel<19>, dim3(c->W), dim3(64), 0, c->stream, c->d_mt,
+                       c->d_mtpos, c->d_hasg, c->d_gauss, c->W, kind, n, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return set_err(OLPE_EHIP, "rng stream: %s", hipGetErrorString(e));
+  return OLPE_OK;
+}
+
+int olpe_trace_enable(olpe_ctx *c, int on) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  c->trace_on = on != 0;
+  return OLPE_OK;
+}
+
+int olpe_trace_read(olpe_ctx *c, double *out) {
+  if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const size_t m = (size_t)c->W * c->trace_iters * kTraceF;
+  if (m) HIPCHK(hipMemcpy(out, c->d_trace, m * 8, hipMemcpyDeviceToHost));
+  return OLPE_OK;
+}
+
+int olpe_sync(olpe_ctx *c) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return OLPE_OK;
+}
+
+int olpe_last_kernel_ms(olpe_ctx *c, double *ms) {
+  if (!c || !ms) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->timed) return set_err(OLPE_ESTATE, "no sampler launch yet");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->ev1));
+  float f = 0.f;
+  HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
+  *ms = f;
+  return OLPE_OK;
+}
+
+}  // extern "C"

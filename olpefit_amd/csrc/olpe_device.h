@@ -1,0 +1,298 @@
+// olpe_device.h -- device building blocks of the gfx950 Gibbs sampler.
+//
+// One walker per 64-lane wavefront.  Everything a walker decides (parameter index,
+// proposal, accept) is wave-uniform; the 64 lanes share the per-pixel work of the
+// model + chi^2 sweep.  References are to the reference checkout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace olpe {
+
+// ---------------------------------------------------------------------------------
+// Parameter layouts (apf_step2.py:108, :215-234; 3body/apf_step2_3body.py:220-295)
+// ---------------------------------------------------------------------------------
+template <int NSRC> struct Layout;
+
+template <> struct Layout<2> {
+  static constexpr int NP = 16, PS = 17;
+  static constexpr int DX = 4, DY = 5, RATIO = 8, OFF = 9;
+  static constexpr int S1X = 10, S1Y = 11, S2X = 12, S2Y = 13, T1 = 14, T2 = 15;
+  static constexpr int BG_QUIRK = 12, BG_FIXED = 9;   // apf_step2.py:120 vs :128
+  // lognorm = [6,7,9,10,11,12,13] (apf_step2.py:217)
+  static constexpr uint32_t LOGMASK = (1u << 6) | (1u << 7) | (1u << 9) | (1u << 10) |
+                                      (1u << 11) | (1u << 12) | (1u << 13);
+  __device__ static constexpr int sx(int s) { return s == 0 ? 0 : 2; }
+  __device__ static constexpr int sy(int s) { return s == 0 ? 1 : 3; }
+  __device__ static constexpr int sa(int s) { return s == 0 ? 6 : 7; }
+};
+
+template <> struct Layout<3> {
+  static constexpr int NP = 19, PS = 20;
+  static constexpr int DX = 6, DY = 7, RATIO = 11, OFF = 12;
+  static constexpr int S1X = 13, S1Y = 14, S2X = 15, S2Y = 16, T1 = 17, T2 = 18;
+  static constexpr int BG_QUIRK = 12, BG_FIXED = 12;  // 3body :121, p[12] is bkgd
+  // lognorm = [8,9,10,12,13,14,15,16] (3body :295)
+  static constexpr uint32_t LOGMASK = (1u << 8) | (1u << 9) | (1u << 10) | (1u << 12) |
+                                      (1u << 13) | (1u << 14) | (1u << 15) | (1u << 16);
+  __device__ static constexpr int sx(int s) { return 2 * s; }
+  __device__ static constexpr int sy(int s) { return 2 * s + 1; }
+  __device__ static constexpr int sa(int s) { return 8 + s; }
+};
+
+// ---------------------------------------------------------------------------------
+// Wave helpers
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double uniform_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return uniform_f64(v);
+}
+
+// ---------------------------------------------------------------------------------
+// MT19937 + NumPy legacy distributions
+// The 624-word key lives in LDS (one slice per wave).  Draws are wave-uniform: a
+// batch of 64 tempered outputs is held one-per-lane in a VGPR and read out with
+// v_readlane, so a draw costs one VALU op plus scalar bookkeeping.
+// ---------------------------------------------------------------------------------
+constexpr int MT_N = 624, MT_M = 397;
+constexpr uint32_t MT_A = 0x9908b0dfu, MT_UP = 0x80000000u, MT_LO = 0x7fffffffu;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+// numpy mt19937_gen, parallelised over 64 lanes.  Pass [i0, i0+64) writes key[i] and
+// reads key[i] / key[i+1] (old) and key[i+397] (old, i < 227) or key[i-227] (new,
+// written by an EARLIER pass since 227 > 64); so 10 ordered passes + the last word
+// reproduce the sequential update exactly.
+__device__ inline void mt_twist(uint32_t *key, int lane) {
+  for (int i0 = 0; i0 < MT_N - 1; i0 += 64) {
+    const int i = i0 + lane;
+    uint32_t ki = 0, ki1 = 0, src = 0;
+    if (i < MT_N - 1) {
+      ki = key[i];
+      ki1 = key[i + 1];
+      src = (i < MT_N - MT_M) ? key[i + MT_M] : key[i - (MT_N - MT_M)];
+    }
+    wave_sync();
+    if (i < MT_N - 1) {
+      const uint32_t y = (ki & MT_UP) | (ki1 & MT_LO);
+      key[i] = src ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+    }
+    wave_sync();
+  }
+  if (lane == 0) {
+    const uint32_t y = (key[MT_N - 1] & MT_UP) | (key[0] & MT_LO);
+    key[MT_N - 1] = key[MT_M - 1] ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+  }
+  wave_sync();
+}
+
+struct MTWave {
+  uint32_t *key;  // LDS, MT_N words
+  int pos;        // numpy state->pos (uniform)
+  int bstart;     // first key index held in `batch`
+  int bsize;      // valid lanes in `batch`
+  uint32_t batch; // tempered key[bstart + lane]
+  int has_gauss;
+  double gauss;
+
+  __device__ void refill(int lane) {
+    if (pos >= MT_N) {
+      mt_twist(key, lane);
+      pos = 0;
+    }
+    const int n = (MT_N - pos) < 64 ? (MT_N - pos) : 64;
+    const uint32_t v = (lane < n) ? key[pos + lane] : 0u;
+    batch = mt_temper(v);
+    bstart = pos;
+    bsize = n;
+  }
+  // mt19937_next
+  __device__ __forceinline__ uint32_t next(int lane) {
+    if (pos - bstart >= bsize) refill(lane);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)batch, pos - bstart);
+    ++pos;
+    return v;
+  }
+  // legacy_double: (a >> 5, b >> 6), exact in f64
+  __device__ __forceinline__ double rand53(int lane) {
+    const uint32_t a = next(lane) >> 5;
+    const uint32_t b = next(lane) >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+  }
+  // legacy_gauss: polar Box-Muller with the cached second deviate
+  __device__ double gauss_next(int lane) {
+    if (has_gauss) {
+      has_gauss = 0;
+      const double t = gauss;
+      gauss = 0.0;
+      return t;
+    }
+    double x1, x2, r2;
+    do {
+      x1 = 2.0 * rand53(lane) - 1.0;
+      x2 = 2.0 * rand53(lane) - 1.0;
+      r2 = x1 * x1 + x2 * x2;
+      r2 = uniform_f64(r2);
+    } while (r2 >= 1.0 || r2 == 0.0);
+    const double f = sqrt(-2.0 * log(r2) / r2);
+    gauss = f * x1;
+    has_gauss = 1;
+    return f * x2;
+  }
+  // randint(0, np): buffered_bounded_masked_uint32 with mask = next pow2 - 1
+  template <int NP> __device__ __forceinline__ int randint(int lane) {
+    constexpr uint32_t rng = NP - 1;
+    constexpr uint32_t m1 = rng | (rng >> 1);
+    constexpr uint32_t m2 = m1 | (m1 >> 2);
+    constexpr uint32_t m3 = m2 | (m2 >> 4);
+    constexpr uint32_t mask = m3 | (m3 >> 8) | (m3 >> 16);
+    uint32_t v;
+    do {
+      v = next(lane) & mask;
+    } while (v > rng);
+    return (int)v;
+  }
+};
+
+// np.random.seed(s): init_genrand (mt19937_seed)
+__device__ inline void mt_seed_serial(uint32_t *key, uint32_t s) {
+  for (int i = 0; i < MT_N; ++i) {
+    key[i] = s;
+    s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(i + 1);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Model pieces (astropy 4.3.1 Gaussian2D.evaluate, functional_models.py:366-381)
+// ---------------------------------------------------------------------------------
+struct Trig {
+  double cost2, sint2, sin2t;
+};
+struct Coef {
+  double a, b, c;
+};
+struct Gauss {
+  double amp, x0, y0;
+  Coef k;
+};
+
+__device__ __forceinline__ Trig make_trig(double th) {
+  const double c = cos(th), s = sin(th);
+  return Trig{c * c, s * s, sin(2. * th)};
+}
+
+__device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t) {
+  const double xstd2 = sx * sx, ystd2 = sy * sy;
+  Coef k;
+  k.a = 0.5 * ((t.cost2 / xstd2) + (t.sint2 / ystd2));
+  k.b = 0.5 * ((t.sin2t / xstd2) - (t.sin2t / ystd2));
+  k.c = 0.5 * ((t.sint2 / xstd2) + (t.cost2 / ystd2));
+  return k;
+}
+
+// Per-step model description: 2*NSRC Gaussians (wide, narrow per source; the order
+// build_2d_gaussian adds them in, apf_step2.py:102) + constant background.
+template <int NSRC> struct ModelDesc {
+  Gauss g[2 * NSRC];
+  double bg;
+};
+
+// Assemble the Gaussians for parameter vector q (accessor) and coefficient sets
+// C1 (narrow: sigma_x, sigma_y, theta) and C2 (wide).  apf_step2.py:95-101, :115-120.
+template <int NSRC, class Q>
+__device__ __forceinline__ ModelDesc<NSRC> make_model(const Q &q, const Coef &C1,
+                                                      const Coef &C2, int bkgd_mode) {
+  using L = Layout<NSRC>;
+  ModelDesc<NSRC> m;
+#pragma unroll
+  for (int s = 0; s < NSRC; ++s) {
+    const double tot = q(L::sa(s)) - q(L::OFF);
+    const double wide = tot * q(L::RATIO);
+    const double narrow = tot - wide;
+    const double xc = q(L::sx(s)), yc = q(L::sy(s));
+    m.g[2 * s] = Gauss{wide, xc + q(L::DX), yc + q(L::DY), C2};
+    m.g[2 * s + 1] = Gauss{narrow, xc, yc, C1};
+  }
+  m.bg = q(bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
+  return m;
+}
+
+// ---------------------------------------------------------------------------------
+// Pixel sweep.  Lane L walks one column j (n >= 64: j = 64*pass + L; n < 64: the
+// wave covers 64/n row groups), so the per-column terms a*dx^2 and b*dx are computed
+// once per step and the row term c*dy^2 is wave-uniform for n >= 64.
+// EXACT evaluation keeps the reference operation order per pixel:
+//   q = ((a*dx^2) + ((b*dx)*dy)) + (c*dy^2);  v = A*exp(-q)
+//   model = ((wide_0 + narrow_0) + (wide_1 + narrow_1) [+ ...]) + bg
+//   t = (D - model) * invE;  acc += t*t   (masked pixels: D = invE = 0)
+// ---------------------------------------------------------------------------------
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const double *D,
+                                              const double *invE, double *out, int n_rt,
+                                              int lane) {
+  constexpr int G = 2 * NSRC;
+  const int n = NT ? NT : n_rt;
+  double acc = 0.0;
+  const int S = n >= 64 ? 1 : 64 / n;       // row groups per wave
+  const int nc = n >= 64 ? 64 : n;          // columns per pass
+  const int grp = lane / nc;
+  const int jl = lane - grp * nc;
+  const bool lane_ok = grp < S;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int j = c0 + jl;
+    const bool act = lane_ok && j < n;
+    const double xj = (double)j;
+    double t1[G], t2[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double xd = xj - m.g[g].x0;
+      t1[g] = m.g[g].k.a * (xd * xd);
+      t2[g] = m.g[g].k.b * xd;
+    }
+    const int jj = act ? j : 0;
+#pragma unroll 2
+    for (int i = grp; i < n; i += S) {
+      const double yi = (double)i;
+      double v[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const double yd = yi - m.g[g].y0;
+        const double qq = (t1[g] + t2[g] * yd) + m.g[g].k.c * (yd * yd);
+        v[g] = m.g[g].amp * exp(-qq);
+      }
+      double mod = v[0] + v[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
+      mod = mod + m.bg;
+      const int idx = i * n + jj;
+      if constexpr (WRITE) {
+        if (act) out[i * n + j] = mod;
+      } else {
+        const double t = (D[idx] - mod) * invE[idx];
+        acc = act ? fma(t, t, acc) : acc;
+      }
+    }
+  }
+  return acc;
+}
+
+}  // namespace olpe

@@ -1,0 +1,51 @@
+// olpe_internal.h -- the context object behind the opaque olpe_ctx handle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+struct olpe_ctx {
+  int device = 0;
+  int n = 0;           // square cutout side
+  int nsrc = 2;
+  int bkgd_mode = 0;
+  int np = 16, ps = 17;
+  int eval_mode = 0;   // OLPE_EVAL_EXACT / OLPE_EVAL_FAST
+  bool lds_img = true; // cutout + 1/err staged in LDS by the sampler
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  double *d_D = nullptr;     // [n*n] data as f64, 0 where masked
+  double *d_invE = nullptr;  // [n*n] 1/err, 0 where masked
+  // walker ensemble
+  int W = 0;
+  bool seeded = false;
+  long long count = 0;
+  double *d_state = nullptr;     // [W][ps]
+  uint32_t *d_tries = nullptr;   // [W][np]
+  uint32_t *d_acc = nullptr;     // [W][np]
+  uint32_t *d_mt = nullptr;      // [W][624]
+  int *d_mtpos = nullptr;        // [W]
+  double *d_gauss = nullptr;     // [W]
+  int *d_hasg = nullptr;         // [W]
+  long long *d_done = nullptr;   // [W]
+  // last launch's chain / trace
+  double *d_chain = nullptr;
+  size_t chain_cap = 0;
+  long long chain_rows = 0;
+  double *d_trace = nullptr;
+  size_t trace_cap = 0;
+  int trace_on = 0;
+  long long trace_iters = 0;
+  // scratch for olpe_model / olpe_chi2_batch
+  double *d_scratch = nullptr, *d_scratch2 = nullptr;
+  size_t scratch_cap = 0, scratch2_cap = 0;
+  // RCCL communicator (olpe_comm.hip)
+  void *comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace olpe {
+int set_err(int code, const char *fmt, ...);
+}
+void olpe_comm_release(olpe_ctx *c);

@@ -1,0 +1,101 @@
+"""Pin the oracle: NumPy restatement vs fixtures produced by the reference's own code
+(tests/golden/make_golden.py executed apf_step2.py / apf_step2_3body.py line ranges
+with astropy 4.3.1).  CPU only.
+
+Tolerances (fp64): model pixels rel 1e-13 of the image peak (transcendental ulps of
+NumPy's SIMD exp/sin/cos between NumPy builds), chi^2 rel 1e-12, trajectories: the
+proposed index and the accept decision must be identical at every iteration, proposal
+values / chi^2 / parameters rel 1e-12.
+"""
+import numpy as np
+import pytest
+
+from oracle import olpe_oracle as ora
+from oracle.legacy_rng import LegacyMT
+
+CASES = ["c32", "c64", "c64_3", "c128_3"]
+
+
+def test_rng_numpy_stream_frozen(golden):
+    g = golden("rng")
+    for i, s in enumerate(g["seeds"]):
+        rs = np.random.RandomState(int(s))
+        assert np.array_equal(rs.randint(0, 2 ** 32, size=1500, dtype=np.uint64), g["raw"][i])
+        assert np.array_equal(np.random.RandomState(int(s)).standard_normal(400), g["gauss"][i])
+        assert np.array_equal(np.random.RandomState(int(s)).rand(400), g["unif"][i])
+
+
+def test_rng_restatement_matches_golden(golden):
+    """Appendix-B restatement (what the HIP kernel implements) is bit-exact."""
+    g = golden("rng")
+    for i, s in enumerate(g["seeds"]):
+        mt = LegacyMT(int(s))
+        assert [mt.next_u32() for _ in range(1500)] == [int(v) for v in g["raw"][i]]
+        mt = LegacyMT(int(s))
+        assert np.array_equal([mt.gauss() for _ in range(400)], g["gauss"][i])
+        mt = LegacyMT(int(s))
+        assert np.array_equal([mt.rand() for _ in range(400)], g["unif"][i])
+        mt = LegacyMT(int(s))
+        assert [mt.randint(16) for _ in range(400)] == list(g["randint16"][i])
+        mt = LegacyMT(int(s))
+        assert [mt.randint(19) for _ in range(400)] == list(g["randint19"][i])
+
+
+def test_first_outputs_known_answers():
+    # first outputs for seeds 0, 1, 5489, 12345, 2**32-1
+    want = {0: 2357136044, 1: 1791095845, 5489: 3499211612, 12345: 3992670690,
+            2 ** 32 - 1: 419326371}
+    for s, v in want.items():
+        assert LegacyMT(s).next_u32() == v
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_noise_model_and_init(golden, name):
+    g = golden(name)
+    img = g["image"]
+    nsrc = int(g["nsrc"])
+    dm, err, sat, rn = ora.noise_model(img, 1.0, 1, 1, 2)
+    assert np.array_equal(np.ma.getmaskarray(dm), g["mask"])
+    assert np.array_equal(err, g["err"])
+    assert sat == g["satlevel"] and rn == g["readnoise"]
+    p0 = ora.initial_parameters(img, g["guess"], nsrc)
+    assert np.array_equal(p0[:-1], g["p_init"][:-1])
+    with np.errstate(all="ignore"):
+        chi = ora.chi_squared(dm, ora.build_analytical_model(p0, img.shape[0], nsrc), err)
+    np.testing.assert_allclose(float(chi), g["p_init"][-1], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_model_and_chi2(golden, name):
+    g = golden(name)
+    img = g["image"]
+    n = img.shape[0]
+    nsrc = int(g["nsrc"])
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    for k, p in enumerate(g["params"]):
+        with np.errstate(all="ignore"):
+            m = ora.build_analytical_model(p, n, nsrc)
+            c = ora.chi_squared(dm, m, err)
+        ref = g["models"][k]
+        scale = np.max(np.abs(ref))
+        assert np.max(np.abs(m - ref)) <= 1e-13 * scale, (name, k)
+        np.testing.assert_allclose(float(c), g["chi2"][k], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_trajectories(golden, name):
+    g = golden(name)
+    img = g["image"]
+    nsrc = int(g["nsrc"])
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    for w, seed in enumerate(g["seeds"]):
+        L = int(g["traj_len"][w])
+        walker = ora.Walker(dm, err, g["p_init"], int(seed), nsrc)
+        for i in range(L):
+            r, new, chi, dice, acc = walker.step()
+            assert r == g["traj_r"][w, i], (name, w, i)
+            assert acc == g["traj_acc"][w, i], (name, w, i)
+            assert dice == g["traj_dice"][w, i]
+            np.testing.assert_allclose(new, g["traj_new"][w, i], rtol=1e-12)
+            np.testing.assert_allclose(chi, g["traj_chi"][w, i], rtol=1e-12)
+            np.testing.assert_allclose(walker.parameters, g["traj_params"][w, i], rtol=1e-12)
