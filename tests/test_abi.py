@@ -1,0 +1,84 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/olpe.h
+declares, the ctypes signatures match the header, and calls fail cleanly (no abort)
+on a host without a GPU.  No compute calls."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from olpefit_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      "include", "olpe.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(olpe_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from olpefit_amd import build
+    build.build(verbose=False)
+    return _lib.load()
+
+
+def test_header_declares_expected_api():
+    names = header_functions()
+    for must in ("olpe_create", "olpe_model", "olpe_chi2_batch", "olpe_seed", "olpe_run",
+                 "olpe_run_gibbs", "olpe_rng_get", "olpe_rng_set", "olpe_destroy",
+                 "olpe_last_error", "olpe_comm_allgather_state"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\sT\s+(olpe_\w+)", out))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+    # ctypes table covers the header one-to-one
+    assert sorted(_lib.SIGNATURES) == header_functions()
+
+
+def test_version_and_device_count(lib):
+    assert lib.olpe_version() >= 100
+    n = C.c_int(-1)
+    assert lib.olpe_device_count(C.byref(n)) == 0
+    assert n.value >= 0
+
+
+def test_create_validates_arguments_before_touching_a_gpu(lib):
+    img = np.zeros((8, 9), np.float32)
+    ctx = C.c_void_p()
+    rc = lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 8, 9, 2, 0, 0,
+                         C.byref(ctx))
+    assert rc == _lib.EINVAL and b"square" in lib.olpe_last_error()
+    img = np.zeros((8, 8), np.float32)
+    assert lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 8, 8, 4, 0, 0,
+                           C.byref(ctx)) == _lib.EINVAL
+    assert lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 8, 8, 2, 0, -1,
+                           C.byref(ctx)) == _lib.EINVAL          # no CPU path
+
+
+def test_no_gpu_fails_loudly(lib):
+    n = C.c_int(0)
+    lib.olpe_device_count(C.byref(n))
+    if n.value:
+        pytest.skip("GPU present")
+    from olpefit_amd.core import OlpeError, Sampler
+    with pytest.raises(OlpeError) as e:
+        Sampler(np.ones((16, 16), np.float32))
+    assert e.value.code == _lib.EHIP
+
+
+def test_null_arguments_are_errors(lib):
+    assert lib.olpe_model(None, None, None) == _lib.EINVAL
+    assert lib.olpe_run(None, 1, 0, 1, 0, None) == _lib.EINVAL
+    assert lib.olpe_sync(None) == _lib.EINVAL
+    lib.olpe_destroy(None)
