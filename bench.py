@@ -1,0 +1,246 @@
+"""Benchmark: walker-steps/s of the apf_step2 Gibbs/MH hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--mode exact|fast]
+
+A bench *step* is one launch of the fused sampler kernel: every walker on the GPU
+runs ``--iters`` Gibbs iterations (apf_step2.py:300-351: parameter draw, proposal,
+full-image model + chi^2, accept/reject), recording its state every ``--stride``
+iterations into an HBM chain buffer.  Inputs (cutout, sigma map, walker state, RNG
+state) are resident in HBM before the timed region.
+
+Workload (BASELINE.json configs[2]): 65,536 walkers per
+GPU on a synthetic 64x64 two-source NIRC2 cutout, fp64, chain stride 10.  For N > 1
+GPUs the driver launches one process per GPU (torch.distributed.run); walkers are
+sharded with seeds 1000 + global walker index, there is no communication while
+sampling, and the end-of-run RCCL all-gather of final states (outside the timed
+region, reported as ``allgather_ms``) is the only exchange.  ``scaling`` is "weak".
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# BASELINE.json configs -> (walkers per GPU, image side, nsrc)
+# (keys are BASELINE.json config indices; [0] is the 1-walker CPU plumbing case and
+# [3] is configs[2] sharded over 8 GPUs, i.e. this bench at --gpus 8)
+CONFIGS = {
+    1: (4096, 64, 2),
+    2: (65536, 64, 2),
+    4: (16384, 128, 3),
+}
+CONFIG_NAMES = {
+    1: "configs[1]: 4,096 walkers, 64x64 2-source cutout, fp64",
+    2: "configs[2]: 65,536 walkers/GPU, 64x64 2-source cutout, fp64, LDS-resident image",
+    4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
+}
+FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
+EXP_OPS = 22                      # FP64 VALU ops of one ocml exp
+
+
+def alg_ops_per_step(n: int, nsrc: int) -> float:
+    """Np*(12G+8) + E*Np*G FP64 lane-ops per walker-step."""
+    npx = n * n
+    g = 2 * nsrc
+    return npx * (12 * g + 8) + EXP_OPS * npx * g
+
+
+# ----------------------------------------------------------------------------------
+# CPU baseline (oracle, one walker per process like one MPI rank per walker)
+# ----------------------------------------------------------------------------------
+def _cpu_worker(args):
+    n, nsrc, seed, iters = args
+    from olpefit_amd import synth
+    from oracle import olpe_oracle as ora
+    img, _ = synth.make_image(n, nsrc, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = ora.initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    w = ora.Walker(dm, err, p0, seed, nsrc)
+    w.init_chi2()
+    t = time.perf_counter()
+    w.run(iters)
+    return time.perf_counter() - t
+
+
+def cpu_baseline(n: int, nsrc: int, iters: int, procs: int):
+    with mp.get_context("spawn").Pool(procs) as pool:
+        pool.map(_cpu_worker, [(n, nsrc, 1, 5)] * procs)          # import warm-up
+        t0 = time.perf_counter()
+        times = pool.map(_cpu_worker, [(n, nsrc, 1000 + i, iters) for i in range(procs)])
+        wall = time.perf_counter() - t0
+    steps = procs * iters
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": steps / wall, "unit": "walker-steps/s", "cores": procs, "kind": "port",
+            "sample": f"oracle/olpe_oracle.py NumPy restatement, {procs} processes x 1 walker "
+                      f"x {iters} iterations, {n}x{n} {nsrc}-source cutout "
+                      f"({sum(times):.1f} s CPU); cpu: {cpu_model or platform.processor()}"}
+
+
+def load_traffic(path: str):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+# ----------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--walkers", type=int, default=0, help="override walkers per GPU")
+    ap.add_argument("--iters", type=int, default=100, help="Gibbs iterations per step")
+    ap.add_argument("--stride", type=int, default=10, help="chain record stride")
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--cpu-iters", type=int, default=2000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import datetime
+
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", rank=rank, world_size=world,
+                                 timeout=datetime.timedelta(minutes=10))
+        dist = tdist
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+
+    wpg, n, nsrc = CONFIGS[args.config]
+    if args.walkers:
+        wpg = args.walkers
+    img, _ = synth.make_image(n, nsrc, 0)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=local)
+    s.set_eval_mode(args.mode)
+    # step-1 style start (apf_step2.py:264-289) for every walker
+    from olpefit_amd.pipeline import initial_parameters
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    p0[-1] = s.chi_squared(p0)
+    seeds = 1000 + rank * wpg + np.arange(wpg)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (wpg, 1)))
+
+    for _ in range(args.warmup):
+        s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+    s.sync()
+    barrier()
+    s.sync()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+        kms.append(s.last_kernel_ms())      # HIP events on the launch stream
+    s.sync()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = allmax(t1 - t0)
+    kernel_ms = float(np.mean(kms))
+
+    # end-of-run exchange: RCCL all-gather of final walker states
+    gather_ms = None
+    if dist:
+        import torch
+        uid = [Sampler.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        s.comm_init(uid[0], world, rank)
+        barrier()
+        tg = time.perf_counter()
+        allst = s.allgather_state()
+        gather_ms = allmax(time.perf_counter() - tg) * 1e3
+        assert allst.shape == (world * wpg, s.ps)
+
+    if rank != 0:
+        s.close()
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    total = world * wpg * args.iters * args.steps
+    value = total / elapsed
+    ops = alg_ops_per_step(n, nsrc)
+    steps_per_launch = wpg * args.iters
+    achieved = steps_per_launch * ops / (kernel_ms * 1e-3) / 1e12
+    traffic = load_traffic(args.traffic)
+    out = {
+        "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "walker-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
+        "config": {"workload": CONFIG_NAMES[args.config], "walkers_per_gpu": wpg,
+                   "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
+                   "chain_stride": args.stride, "eval": args.mode,
+                   "parallelism": f"walker-sharded x{world}"},
+        "roofline": {
+            "bound": "fp64-valu",
+            "achieved": achieved / 1.0,
+            "peak": FP64_LANE_PEAK / 1e12,
+            "unit": "TFLOP/s",
+            "frac": achieved / (FP64_LANE_PEAK / 1e12),
+            "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "kernel": "olpe_gibbs_kernel",
+            "kernel_ms": kernel_ms,
+            "work_per_walker_step": ops,
+            "note": "FP64 VALU lane-ops (FMA counted once) of the reference algorithm, "
+                    "SURVEY.md §8(d) with E=22; peak = 78.6 TFLOP/s / 2; DESIGN.md §4",
+        },
+        "allgather_ms": gather_ms,
+    }
+    if not args.no_cpu_baseline and world == 1:
+        procs = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(n, nsrc, args.cpu_iters, procs)
+    print(json.dumps(out))
+    s.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,104 @@
+"""The step1 -> step2 -> step3 file surface kept by the build.
+
+* step-1 guess file ``<dir>/<frame>_initialguess`` (apf_step1.py:166-175), read with
+  ``np.loadtxt`` (apf_step2.py:261-262)
+* initial parameter vector (apf_step2.py:264-273; 3body/apf_step2_3body.py:255-265)
+* step-2a warm start: last row of ``step2a.csv`` (apf_step2.py:248-256)
+* chain files ``{rank}_finalarray_mpi.csv``: ``csv.writer`` rows, NaN first row,
+  PS columns (apf_step2.py:278-279, :342-360), and ``{rank}_acceptance_rate.csv`` =
+  ``str(total_accept / total_tries)`` (:362-365)
+* output directory ``<dir>/<frame>_apf_results/`` where ``<frame>`` is
+  ``basename.split('.')[-3]`` (apf_step2.py:164-173)
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+SIGMA0 = (50 / 9.95) / 2.35   # apf_step2.py:242-245
+
+
+def image_paths(image_path: str):
+    """(directory, frame, output_directory) exactly as apf_step2.py:164-170 builds
+    them (string concatenation on '/')."""
+    d = image_path.split('/')
+    directory = ''
+    for i in range(len(d) - 1):
+        directory = directory + str(d[i]) + '/'
+    frame = d[-1].split('.')[-3]
+    return directory, frame, directory + frame + '_apf_results/'
+
+
+def read_guess(path: str):
+    """apf_step2.py:262: ``np.loadtxt(open(fileguess, "rb"), delimiter=' ')``."""
+    with open(path, "rb") as f:
+        return np.loadtxt(f, delimiter=' ')
+
+
+def initial_parameters(image, guess, nsrc: int = 2):
+    """apf_step2.py:264-273 (2 sources) / 3body :255-265 (3 sources).  The chi^2 slot
+    is 0; apf_step2.py:283-289 fills it with the initial chi^2."""
+    sigma = SIGMA0
+    if nsrc == 2:
+        xcs, ycs, xcc, ycc = guess[0], guess[1], guess[2], guess[3]
+        amps = image[int(ycs - 1), int(xcs - 1)]
+        ampc = image[int(ycc - 1), int(xcc - 1)]
+        box = image[int(guess[5]):int(guess[5]) + 10, int(guess[4]):int(guess[4]) + 10]
+        bkgd = np.median(box)
+        return np.array([xcs, ycs, xcc, ycc, 0., 0., amps, ampc, 0.2, bkgd, sigma, sigma,
+                         sigma * 3, sigma * 3, 0., 0., 0.], dtype=np.float64)
+    xca, yca, xcb, ycb, xcc, ycc = (guess[k] for k in range(6))
+    ampa = image[int(yca - 0.5 + 1), int(xca - 0.5 + 1)]
+    ampb = image[int(ycb - 0.5 + 1), int(xcb - 0.5 + 1)]
+    ampc = image[int(ycc - 0.5 + 1), int(xcc - 0.5 + 1)]
+    box = image[int(guess[7]):int(guess[7]) + 10, int(guess[6]):int(guess[6]) + 10]
+    bkgd = np.median(box)
+    return np.array([xca, yca, xcb, ycb, xcc, ycc, 0., 0., ampa, ampb, ampc, 0.2, bkgd,
+                     sigma, sigma, sigma * 3, sigma * 3, 0., 0., 0.], dtype=np.float64)
+
+
+def read_step2a(path: str):
+    """apf_step2.py:253-256: ``genfromtxt(step2a.csv)[-1:][0]``."""
+    a = np.genfromtxt(path, delimiter=',')
+    return np.atleast_2d(a)[-1:][0]
+
+
+def format_rows(chain) -> str:
+    """CSV text ``csv.writer`` produces for ``writerows(rows)`` of float rows: ','
+    separator, '\\r\\n' terminator, shortest-repr floats, NaN as 'nan'."""
+    lines = [",".join([repr(v) for v in row]) for row in np.asarray(chain, dtype=np.float64).tolist()]
+    return "".join(line + "\r\n" for line in lines)
+
+
+def write_chain_csv(path: str, rows) -> None:
+    """``{rank}_finalarray_mpi.csv``: ``rows`` must already hold the NaN seed row."""
+    with open(path, "w", newline="") as f:
+        f.write(format_rows(rows))
+
+
+def with_seed_row(chain):
+    """Prepend the all-NaN row the reference starts ``total_parameters`` with
+    (apf_step2.py:278-279)."""
+    chain = np.asarray(chain, dtype=np.float64)
+    return np.vstack([np.full((1, chain.shape[-1]), np.nan), chain.reshape(-1, chain.shape[-1])])
+
+
+def acceptance_text(accepts, tries) -> str:
+    """apf_step2.py:363-364: ``str(total_accept / total_tries)``."""
+    with np.errstate(all="ignore"):
+        return str(np.asarray(accepts, dtype=np.float64) / np.asarray(tries, dtype=np.float64))
+
+
+def write_acceptance(path: str, accepts, tries) -> None:
+    with open(path, "w") as f:
+        f.write(acceptance_text(accepts, tries))
+
+
+def written_rows(count: int, burn_in: int) -> int:
+    """Data rows on disk after ``count`` iterations: the reference appends a row every
+    iteration with count >= burn_in but rewrites the file only when count % 10 == 0
+    (apf_step2.py:342-360), so the file holds rows up to the last multiple of 10."""
+    last = (count // 10) * 10
+    first = max(burn_in, 1)          # count is incremented before the burn-in check
+    return last - first + 1 if last >= first else 0
