@@ -42,10 +42,10 @@ template <int NSRC> __device__ __forceinline__ double width_of(int r) {
 }
 
 struct GibbsArgs {
-  const double *D;     // [n*n] f64 data (0 where masked)
-  const double *invE;  // [n*n] 1/err (0 where masked)
+  const double2 *DE;   // [n*n] {data, 1/err} ({0,0} where masked)
   int n;
   int bkgd_mode;
+  int fast;            // OLPE_EVAL_FAST
   long long W;
   double *state;       // [W][PS]
   uint32_t *tries;     // [W][NP]
@@ -79,8 +79,10 @@ template <int NP> struct WaveSlice {
   static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
   static constexpr int OPT = PS + 12, OPC = PS + 15;
   static constexpr int F64 = PS + 18;
-  static constexpr int BYTES = U32 * 4 + F64 * 8;
+  static constexpr int BYTES = (U32 * 4 + F64 * 8 + 15) & ~15;   // + V table (per n)
 };
+// bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
+__host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
@@ -103,36 +105,23 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
 
-  // ---- LDS carve: [D | invE] (if staged) then one WaveSlice per wave
-  const int npad = (npix + 1) & ~1;   // keep sE 16-byte aligned
-  double *sD = reinterpret_cast<double *>(smem);
-  double *sE = sD + (LDS_IMG ? npad : 0);
-  unsigned char *wb = reinterpret_cast<unsigned char *>(sE + (LDS_IMG ? npad : 0)) +
-                      (size_t)wave * WS::BYTES;
+  // ---- LDS carve: [DE] (if staged) then one {WaveSlice, V table} per wave
+  double2 *sDE = reinterpret_cast<double2 *>(smem);
+  const int wstride = WS::BYTES + vtab_bytes(n, NSRC);
+  unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
+                      (size_t)wave * wstride;
   uint32_t *key = reinterpret_cast<uint32_t *>(wb);
   uint32_t *s_tries = key + MT_N;
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
+  double *vtab = reinterpret_cast<double *>(wb + WS::BYTES);
 
   if constexpr (LDS_IMG) {
-    // one coalesced 16-B-per-lane staging pass of the cutout and 1/err
-    const int nv = npix / 2;
-    const double2 *gD = reinterpret_cast<const double2 *>(A.D);
-    const double2 *gE = reinterpret_cast<const double2 *>(A.invE);
-    double2 *lD = reinterpret_cast<double2 *>(sD);
-    double2 *lE = reinterpret_cast<double2 *>(sE);
-    for (int k = threadIdx.x; k < nv; k += blockDim.x) {
-      lD[k] = gD[k];
-      lE[k] = gE[k];
-    }
-    if ((npix & 1) && threadIdx.x == 0) {
-      sD[npix - 1] = A.D[npix - 1];
-      sE[npix - 1] = A.invE[npix - 1];
-    }
+    // one coalesced 16-B-per-lane staging pass of {data, 1/err}
+    for (int k = threadIdx.x; k < npix; k += blockDim.x) sDE[k] = A.DE[k];
     __syncthreads();
   }
-  const double *D = LDS_IMG ? sD : A.D;
-  const double *invE = LDS_IMG ? sE : A.invE;
+  const double2 *DE = LDS_IMG ? sDE : A.DE;
 
   const long long w = (long long)blockIdx.x * WPB + wave;
   if (w >= A.W) return;
@@ -215,7 +204,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     const ModelDesc<NSRC> md = make_model<NSRC>(q, C1p, C2p, A.bkgd_mode);
 
     // build_analytical_model + chi_squared (:314-316)
-    const double part = sweep_exact<NSRC, NT, false>(md, D, invE, nullptr, n, lane);
+    const double part = sweep<NSRC, NT, false>(md, DE, vtab, nullptr, n, lane, A.fast != 0);
     const double chi = wave_sum(part);
 
     // accept_reject (:139-148)
@@ -274,14 +263,16 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
 // Model / chi^2 of explicit parameter vectors (one wave per vector; image in global)
 // ---------------------------------------------------------------------------------
 template <int NSRC, bool WRITE>
-__global__ __launch_bounds__(256) void olpe_eval_kernel(const double *D, const double *invE,
-                                                        int n, int bkgd_mode,
-                                                        const double *params, int W,
+__global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n, int bkgd_mode,
+                                                        int fast, const double *params, int W,
                                                         double *out) {
   using L = Layout<NSRC>;
   constexpr int PS = L::PS;
+  extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
-  const long long w = (long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int wave = threadIdx.x >> 6;
+  double *vtab = reinterpret_cast<double *>(smem + (size_t)wave * vtab_bytes(n, NSRC));
+  const long long w = (long long)blockIdx.x * (blockDim.x / 64) + wave;
   if (w >= W) return;
   double p[PS];
 #pragma unroll
@@ -292,9 +283,9 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double *D, const d
   auto q = [&](int k) -> double { return p[k]; };
   const ModelDesc<NSRC> md = make_model<NSRC>(q, C1, C2, bkgd_mode);
   if constexpr (WRITE) {
-    sweep_exact<NSRC, 0, true>(md, D, invE, out + (size_t)w * n * n, n, lane);
+    sweep<NSRC, 0, true>(md, DE, vtab, out + (size_t)w * n * n, n, lane, fast != 0);
   } else {
-    const double chi = wave_sum(sweep_exact<NSRC, 0, false>(md, D, invE, nullptr, n, lane));
+    const double chi = wave_sum(sweep<NSRC, 0, false>(md, DE, vtab, nullptr, n, lane, fast != 0));
     if (lane == 0) out[w] = chi;
   }
 }
@@ -392,9 +383,14 @@ template <class T> int dev_alloc(T **p, size_t count) {
   return OLPE_OK;
 }
 
+size_t wave_lds(int n, int np) {
+  return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) +
+         vtab_bytes(n, np == 16 ? 2 : 3);
+}
+
 size_t lds_bytes(const olpe_ctx *c, int wpb) {
-  size_t b = (size_t)wpb * (c->np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES);
-  if (c->lds_img) b += (size_t)((c->n * c->n + 1) & ~1) * 2 * sizeof(double);
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np);
+  if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   return b;
 }
 
@@ -457,7 +453,7 @@ int ensure_ensemble(olpe_ctx *c, int W) {
 
 extern "C" {
 
-int olpe_version(void) { return 100; }
+int olpe_version(void) { return 101; }
 
 const char *olpe_last_error(void) { return g_err; }
 
@@ -501,23 +497,19 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->ps = c->np + 1;
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
-  const size_t slice = c->np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES;
-  c->lds_img = (((npix + 1) & ~(size_t)1) * 16 + 16 * slice) <= 160 * 1024;
+  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) <= 160 * 1024;
 
-  std::vector<double> hD(npix), hE(npix);
+  std::vector<double2> hDE(npix);
   for (size_t i = 0; i < npix; ++i) {
     const double d = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)image)[i]
                                                    : ((const double *)image)[i];
     const double p2 = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)pois2)[i]
                                                     : ((const double *)pois2)[i];
     const double e = sqrt(readnoise2 + p2);   // apf_step2.py:210
-    if (mask && mask[i]) {
-      hD[i] = 0.0;
-      hE[i] = 0.0;
-    } else {
-      hD[i] = d;
-      hE[i] = 1.0 / e;
-    }
+    if (mask && mask[i])
+      hDE[i] = make_double2(0.0, 0.0);
+    else
+      hDE[i] = make_double2(d, 1.0 / e);
   }
   int rc;
   hipError_t e1 = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -527,16 +519,14 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   }
   (void)hipEventCreate(&c->ev0);
   (void)hipEventCreate(&c->ev1);
-  if ((rc = dev_alloc(&c->d_D, npix)) || (rc = dev_alloc(&c->d_invE, npix))) {
+  if ((rc = dev_alloc(&c->d_DE, npix))) {
     olpe_destroy(c);
     return rc;
   }
-  hipError_t e2 = hipMemcpy(c->d_D, hD.data(), npix * 8, hipMemcpyHostToDevice);
-  hipError_t e3 = hipMemcpy(c->d_invE, hE.data(), npix * 8, hipMemcpyHostToDevice);
-  if (e2 != hipSuccess || e3 != hipSuccess) {
+  hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
+  if (e2 != hipSuccess) {
     olpe_destroy(c);
-    return set_err(OLPE_EHIP, "hipMemcpy image: %s",
-                   hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+    return set_err(OLPE_EHIP, "hipMemcpy image: %s", hipGetErrorString(e2));
   }
   *out = c;
   return OLPE_OK;
@@ -547,7 +537,7 @@ void olpe_destroy(olpe_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   olpe_comm_release(c);
-  void *ptrs[] = {c->d_D,  c->d_invE,  c->d_state, c->d_tries, c->d_acc,
+  void *ptrs[] = {c->d_DE, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2};
   for (void *p : ptrs)
@@ -580,20 +570,23 @@ static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, boo
   HIPCHK(hipMemcpyAsync(c->d_scratch, params, pin * 8, hipMemcpyHostToDevice, c->stream));
   const int wpb = 4;
   dim3 grid((W + wpb - 1) / wpb), block(wpb * 64);
+  const size_t shm = (size_t)wpb * vtab_bytes(c->n, c->nsrc);
+  const int fast = c->eval_mode == OLPE_EVAL_FAST;
+  if (shm > 65536) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
   if (c->nsrc == 2) {
     if (write)
-      hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, 0, c->stream, c->d_D,
-                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+      hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, shm, c->stream, c->d_DE,
+                         c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
     else
-      hipLaunchKernelGGL((olpe_eval_kernel<2, false>), grid, block, 0, c->stream, c->d_D,
-                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+      hipLaunchKernelGGL((olpe_eval_kernel<2, false>), grid, block, shm, c->stream, c->d_DE,
+                         c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
   } else {
     if (write)
-      hipLaunchKernelGGL((olpe_eval_kernel<3, true>), grid, block, 0, c->stream, c->d_D,
-                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+      hipLaunchKernelGGL((olpe_eval_kernel<3, true>), grid, block, shm, c->stream, c->d_DE,
+                         c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
     else
-      hipLaunchKernelGGL((olpe_eval_kernel<3, false>), grid, block, 0, c->stream, c->d_D,
-                         c->d_invE, c->n, c->bkgd_mode, c->d_scratch, W, c->d_scratch2);
+      hipLaunchKernelGGL((olpe_eval_kernel<3, false>), grid, block, shm, c->stream, c->d_DE,
+                         c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->d_scratch2, pout * 8, hipMemcpyDeviceToHost, c->stream));
@@ -712,8 +705,8 @@ int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_strid
   c->trace_iters = c->trace_on ? n_iters : 0;
 
   GibbsArgs a;
-  a.D = c->d_D;
-  a.invE = c->d_invE;
+  a.DE = c->d_DE;
+  a.fast = c->eval_mode == OLPE_EVAL_FAST;
   a.n = c->n;
   a.bkgd_mode = c->bkgd_mode;
   a.W = c->W;

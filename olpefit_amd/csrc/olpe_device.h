@@ -237,29 +237,37 @@ __device__ __forceinline__ ModelDesc<NSRC> make_model(const Q &q, const Coef &C1
 }
 
 // ---------------------------------------------------------------------------------
-// Pixel sweep.  Lane L walks one column j (n >= 64: j = 64*pass + L; n < 64: the
-// wave covers 64/n row groups), so the per-column terms a*dx^2 and b*dx are computed
-// once per step and the row term c*dy^2 is wave-uniform for n >= 64.
+// Pixel sweeps.  The cutout is stored interleaved, DE[pixel] = {D, 1/err} (one
+// ds_read_b128 per pixel; masked pixels hold {0, 0}).  Lane L walks one column j
+// (n >= 64: j = 64*pass + L; n < 64: the wave covers 64/n row groups, stride S), so
+// per-column terms are computed once per step.
+// ---------------------------------------------------------------------------------
+struct ColWalk {
+  int S, nc, grp, jl;
+  bool lane_ok;
+  __device__ __forceinline__ ColWalk(int n, int lane) {
+    S = n >= 64 ? 1 : 64 / n;      // row groups per wave
+    nc = n >= 64 ? 64 : n;         // columns per pass
+    grp = lane / nc;
+    jl = lane - grp * nc;
+    lane_ok = grp < S;
+  }
+};
+
 // EXACT evaluation keeps the reference operation order per pixel:
 //   q = ((a*dx^2) + ((b*dx)*dy)) + (c*dy^2);  v = A*exp(-q)
 //   model = ((wide_0 + narrow_0) + (wide_1 + narrow_1) [+ ...]) + bg
-//   t = (D - model) * invE;  acc += t*t   (masked pixels: D = invE = 0)
-// ---------------------------------------------------------------------------------
+//   t = (D - model) * invE;  acc += t*t
 template <int NSRC, int NT, bool WRITE>
-__device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const double *D,
-                                              const double *invE, double *out, int n_rt,
-                                              int lane) {
+__device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const double2 *DE,
+                                              double *out, int n_rt, int lane) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
+  const ColWalk cw(n, lane);
   double acc = 0.0;
-  const int S = n >= 64 ? 1 : 64 / n;       // row groups per wave
-  const int nc = n >= 64 ? 64 : n;          // columns per pass
-  const int grp = lane / nc;
-  const int jl = lane - grp * nc;
-  const bool lane_ok = grp < S;
   for (int c0 = 0; c0 < n; c0 += 64) {
-    const int j = c0 + jl;
-    const bool act = lane_ok && j < n;
+    const int j = c0 + cw.jl;
+    const bool act = cw.lane_ok && j < n;
     const double xj = (double)j;
     double t1[G], t2[G];
 #pragma unroll
@@ -270,7 +278,7 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
     }
     const int jj = act ? j : 0;
 #pragma unroll 2
-    for (int i = grp; i < n; i += S) {
+    for (int i = cw.grp; i < n; i += cw.S) {
       const double yi = (double)i;
       double v[G];
 #pragma unroll
@@ -283,16 +291,115 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
 #pragma unroll
       for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
       mod = mod + m.bg;
-      const int idx = i * n + jj;
       if constexpr (WRITE) {
         if (act) out[i * n + j] = mod;
       } else {
-        const double t = (D[idx] - mod) * invE[idx];
+        const double2 de = DE[i * n + jj];
+        const double t = (de.x - mod) * de.y;
         acc = act ? fma(t, t, acc) : acc;
       }
     }
   }
   return acc;
+}
+
+// FAST evaluation: with dx = j - x0, dy = i - y0,
+//   A*exp(-(a dx^2 + b dx dy + c dy^2)) = (U_j * V_i) * W_ij
+//   U_j = exp(-a dx^2)            one exp per lane (column), per step
+//   V_i = A * exp(-c dy^2)        one exp per lane (row), per step, kept in LDS
+//   W_ij = exp(-b dx dy)          W_(i+S) = W_ij * exp(-b dx S): one multiply
+// so a pixel-Gaussian costs 3 multiplies instead of an exp.  Valid while the cross
+// term stays bounded (|b dx dy| < kFastCross over the grid): then U*V can only
+// underflow where the Gaussian is < e^-400 anyway.  Otherwise (or for non-finite
+// parameters) the exact sweep runs -- a wave-uniform decision.
+constexpr double kFastCross = 300.0;
+
+template <int NSRC>
+__device__ __forceinline__ bool fast_ok(const ModelDesc<NSRC> &m, int n) {
+  bool ok = true;
+  const double hi = (double)(n - 1);
+#pragma unroll
+  for (int g = 0; g < 2 * NSRC; ++g) {
+    const Gauss &q = m.g[g];
+    const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
+    const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
+    const double B = fabs(q.k.b) * mx * my;
+    ok = ok && (B < kFastCross) && isfinite(q.k.a) && isfinite(q.k.c) && isfinite(q.amp) &&
+         (q.k.a >= 0.0) && (q.k.c >= 0.0);
+  }
+  return ok;
+}
+
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const double2 *DE,
+                                             double *vtab, double *out, int n_rt,
+                                             int lane) {
+  constexpr int G = 2 * NSRC;
+  const int n = NT ? NT : n_rt;
+  const ColWalk cw(n, lane);
+  // row table V[i][g] = A_g * exp(-c_g dy^2), rows lane-parallel
+  for (int i = lane; i < n; i += 64) {
+    const double yi = (double)i;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double yd = yi - m.g[g].y0;
+      vtab[i * G + g] = m.g[g].amp * exp(-(m.g[g].k.c * (yd * yd)));
+    }
+  }
+  wave_sync();
+  double acc = 0.0;
+  const double S = (double)cw.S;
+  const double y0r = (double)cw.grp;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int j = c0 + cw.jl;
+    const bool act = cw.lane_ok && j < n;
+    const double xj = (double)j;
+    double U[G], E[G], Wc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double xd = xj - m.g[g].x0;
+      const double bx = m.g[g].k.b * xd;
+      U[g] = exp(-(m.g[g].k.a * (xd * xd)));
+      E[g] = exp(-(bx * S));
+      Wc[g] = exp(-(bx * (y0r - m.g[g].y0)));
+    }
+    const int jj = act ? j : 0;
+#pragma unroll 2
+    for (int i = cw.grp; i < n; i += cw.S) {
+      const double2 *vr = reinterpret_cast<const double2 *>(vtab + i * G);
+      double v[G];
+#pragma unroll
+      for (int h = 0; h < G / 2; ++h) {
+        const double2 vv = vr[h];
+        v[2 * h] = (U[2 * h] * vv.x) * Wc[2 * h];
+        v[2 * h + 1] = (U[2 * h + 1] * vv.y) * Wc[2 * h + 1];
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) Wc[g] = Wc[g] * E[g];
+      double mod = v[0] + v[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
+      mod = mod + m.bg;
+      if constexpr (WRITE) {
+        if (act) out[i * n + j] = mod;
+      } else {
+        const double2 de = DE[i * n + jj];
+        const double t = (de.x - mod) * de.y;
+        acc = act ? fma(t, t, acc) : acc;
+      }
+    }
+  }
+  wave_sync();   // vtab is rewritten by the next step
+  return acc;
+}
+
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *DE,
+                                        double *vtab, double *out, int n, int lane,
+                                        bool fast) {
+  if (fast && fast_ok<NSRC>(m, NT ? NT : n))
+    return sweep_fast<NSRC, NT, WRITE>(m, DE, vtab, out, n, lane);
+  return sweep_exact<NSRC, NT, WRITE>(m, DE, out, n, lane);
 }
 
 }  // namespace olpe

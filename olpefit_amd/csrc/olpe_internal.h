@@ -15,8 +15,7 @@ struct olpe_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
-  double *d_D = nullptr;     // [n*n] data as f64, 0 where masked
-  double *d_invE = nullptr;  // [n*n] 1/err, 0 where masked
+  double2 *d_DE = nullptr;   // [n*n] {data as f64, 1/err}, {0,0} where masked
   // walker ensemble
   int W = 0;
   bool seeded = false;
