@@ -46,14 +46,26 @@ CONFIG_NAMES = {
     4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
 }
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
-EXP_OPS = 22                      # FP64 VALU ops of one ocml exp
+EXP_OPS = 20                      # FP64 VALU ops of one ocml exp(f64)
 
 
-def alg_ops_per_step(n: int, nsrc: int) -> float:
-    """Np*(12G+8) + E*Np*G FP64 lane-ops per walker-step."""
-    npx = n * n
+def work_per_step(n: int, nsrc: int, mode: str) -> float:
+    """FP64 VALU lane-ops of one walker-step's model + chi^2 evaluation.
+
+    exact: per pixel-Gaussian 7 ops + one exp, per pixel G-1 combines + background +
+           3 residual ops, per column-Gaussian 4 hoisted ops.
+    fast:  per pixel-Gaussian 3 multiplies (+1 combine), per pixel 3 residual ops,
+           per Gaussian 4 exps per row/column (U, E, W0, V) with ~4 ops each."""
     g = 2 * nsrc
-    return npx * (12 * g + 8) + EXP_OPS * npx * g
+    if mode == "exact":
+        return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
+    return n * n * (4 * g + 3) + 4 * n * g * (EXP_OPS + 4)
+
+
+def sec8d_work(n: int, nsrc: int) -> float:
+    """SURVEY.md §8(d)'s exp-form count Np*(12G+8) + E*Np*G (reference formula)."""
+    g = 2 * nsrc
+    return n * n * (12 * g + 8) + EXP_OPS * n * n * g
 
 
 # ----------------------------------------------------------------------------------
@@ -113,7 +125,9 @@ def main():
     ap.add_argument("--walkers", type=int, default=0, help="override walkers per GPU")
     ap.add_argument("--iters", type=int, default=100, help="Gibbs iterations per step")
     ap.add_argument("--stride", type=int, default=10, help="chain record stride")
-    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--mode", default="fast", choices=["exact", "fast"])
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the single-GPU measurement of the other eval mode")
     ap.add_argument("--cpu-iters", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -151,7 +165,6 @@ def main():
         wpg = args.walkers
     img, _ = synth.make_image(n, nsrc, 0)
     s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=local)
-    s.set_eval_mode(args.mode)
     # step-1 style start (apf_step2.py:264-289) for every walker
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
@@ -160,21 +173,30 @@ def main():
     s.seed(seeds)
     s.set_state(np.tile(p0, (wpg, 1)))
 
-    for _ in range(args.warmup):
-        s.run_async(args.iters, burn_in=0, record_stride=args.stride)
-    s.sync()
-    barrier()
-    s.sync()
-    t0 = time.perf_counter()
-    kms = []
-    for _ in range(args.steps):
-        s.run_async(args.iters, burn_in=0, record_stride=args.stride)
-        kms.append(s.last_kernel_ms())      # HIP events on the launch stream
-    s.sync()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = allmax(t1 - t0)
-    kernel_ms = float(np.mean(kms))
+    def measure(mode, steps, warmup):
+        s.set_eval_mode(mode)
+        for _ in range(warmup):
+            s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+        s.sync()
+        barrier()
+        s.sync()
+        t0 = time.perf_counter()
+        kms = []
+        for _ in range(steps):
+            s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+            kms.append(s.last_kernel_ms())      # HIP events on the launch stream
+        s.sync()
+        barrier()
+        t1 = time.perf_counter()
+        return allmax(t1 - t0), float(np.mean(kms))
+
+    elapsed, kernel_ms = measure(args.mode, args.steps, args.warmup)
+    alt = None
+    if world == 1 and not args.no_alt:
+        other = "exact" if args.mode == "fast" else "fast"
+        alt_steps = max(2, args.steps // 2)
+        e2, k2 = measure(other, alt_steps, 1)
+        alt = (other, alt_steps, e2, k2)
 
     # end-of-run exchange: RCCL all-gather of final walker states
     gather_ms = None
@@ -197,10 +219,30 @@ def main():
 
     total = world * wpg * args.iters * args.steps
     value = total / elapsed
-    ops = alg_ops_per_step(n, nsrc)
     steps_per_launch = wpg * args.iters
-    achieved = steps_per_launch * ops / (kernel_ms * 1e-3) / 1e12
     traffic = load_traffic(args.traffic)
+
+    def roofline(mode, kernel_ms):
+        ops = work_per_step(n, nsrc, mode)
+        achieved = steps_per_launch * ops / (kernel_ms * 1e-3) / 1e12
+        return {
+            "bound": "fp64-valu",
+            "achieved": achieved,
+            "peak": FP64_LANE_PEAK / 1e12,
+            "unit": "TFLOP/s",
+            "frac": achieved / (FP64_LANE_PEAK / 1e12),
+            "traffic": (traffic or {}).get(mode, {}).get("bytes_per_launch"),
+            "kernel": "olpe_gibbs_kernel",
+            "kernel_ms": kernel_ms,
+            "work_per_walker_step": ops,
+            "walker_steps_per_launch": steps_per_launch,
+            "sec8d_exp_form_equiv": steps_per_launch * sec8d_work(n, nsrc) / (kernel_ms * 1e-3) / 1e12,
+            "note": "FP64 VALU lane-ops (FMA counted once) of the eval algorithm per "
+                    "walker-step x walker-steps per launch / HIP-event kernel time; "
+                    "peak = 78.6 TFLOP/s / 2; traffic = PMC FETCH_SIZE*2 + WRITE_SIZE "
+                    "bytes per launch (profiles/pmc_traffic.json); DESIGN.md §4",
+        }
+
     out = {
         "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
         "value": value,
@@ -218,21 +260,15 @@ def main():
                    "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                    "chain_stride": args.stride, "eval": args.mode,
                    "parallelism": f"walker-sharded x{world}"},
-        "roofline": {
-            "bound": "fp64-valu",
-            "achieved": achieved / 1.0,
-            "peak": FP64_LANE_PEAK / 1e12,
-            "unit": "TFLOP/s",
-            "frac": achieved / (FP64_LANE_PEAK / 1e12),
-            "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "kernel": "olpe_gibbs_kernel",
-            "kernel_ms": kernel_ms,
-            "work_per_walker_step": ops,
-            "note": "FP64 VALU lane-ops (FMA counted once) of the reference algorithm, "
-                    "SURVEY.md §8(d) with E=22; peak = 78.6 TFLOP/s / 2; DESIGN.md §4",
-        },
+        "roofline": roofline(args.mode, kernel_ms),
         "allgather_ms": gather_ms,
     }
+    if alt:
+        other, alt_steps, e2, k2 = alt
+        out["alt_eval"] = {"eval": other,
+                           "value": world * wpg * args.iters * alt_steps / e2,
+                           "ms_per_step": e2 / alt_steps * 1e3,
+                           "roofline": roofline(other, k2)}
     if not args.no_cpu_baseline and world == 1:
         procs = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(n, nsrc, args.cpu_iters, procs)

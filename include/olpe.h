@@ -39,7 +39,7 @@ extern "C" {
 #define OLPE_DTYPE_F64 1
 
 #define OLPE_EVAL_EXACT 0 /* one exp per pixel-Gaussian, reference op order */
-#define OLPE_EVAL_FAST 1  /* separable/recurrence evaluation */
+#define OLPE_EVAL_FAST 1  /* separable exps + cross-term recurrence (default) */
 
 typedef struct olpe_ctx olpe_ctx;
 
@@ -68,7 +68,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
                 const uint8_t *mask, int ny, int nx, int nsrc, int bkgd_mode, int device,
                 olpe_ctx **out);
 void olpe_destroy(olpe_ctx *ctx);
-/* Select OLPE_EVAL_EXACT (default) or OLPE_EVAL_FAST for the sampler. */
+/* Select OLPE_EVAL_FAST (default) or OLPE_EVAL_EXACT for every evaluation of ctx. */
 int olpe_set_eval_mode(olpe_ctx *ctx, int mode);
 
 /* build_analytical_model (apf_step2.py:106-124; 3body :106-125): one PS-vector ->

@@ -14,6 +14,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -45,7 +46,6 @@ struct GibbsArgs {
   const double2 *DE;   // [n*n] {data, 1/err} ({0,0} where masked)
   int n;
   int bkgd_mode;
-  int fast;            // OLPE_EVAL_FAST
   long long W;
   double *state;       // [W][PS]
   uint32_t *tries;     // [W][NP]
@@ -72,14 +72,17 @@ constexpr int kTraceF = 6;
 // The fused sampler
 // ---------------------------------------------------------------------------------
 // Per-wave LDS slice: MT key[624] | tries[NP] | accepts[NP] | state doubles (below)
+// | per-step model descriptor | (after BYTES) the V table of sweep_fast
 template <int NP> struct WaveSlice {
   static constexpr int U32 = MT_N + 2 * NP;                  // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
+  static constexpr int NSRC = NP == 16 ? 2 : 3;
   // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
   static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
   static constexpr int OPT = PS + 12, OPC = PS + 15;
   static constexpr int F64 = PS + 18;
-  static constexpr int BYTES = (U32 * 4 + F64 * 8 + 15) & ~15;   // + V table (per n)
+  static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
+  static constexpr int BYTES = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
 };
 // bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
 __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
@@ -94,7 +97,7 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
   s[0] = k.a; s[1] = k.b; s[2] = k.c;
 }
 
-template <int NSRC, int NT, bool LDS_IMG, int WPB>
+template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
@@ -103,7 +106,8 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   const int n = NT ? NT : A.n;
   const int npix = n * n;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave index as a provably uniform (SGPR) value: LDS slice addresses stay scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
   // ---- LDS carve: [DE] (if staged) then one {WaveSlice, V table} per wave
   double2 *sDE = reinterpret_cast<double2 *>(smem);
@@ -115,6 +119,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
   double *vtab = reinterpret_cast<double *>(wb + WS::BYTES);
+  ModelDesc<NSRC> *mdl = reinterpret_cast<ModelDesc<NSRC> *>(wb + WS::OMD);
 
   if constexpr (LDS_IMG) {
     // one coalesced 16-B-per-lane staging pass of {data, 1/err}
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     double nv;
     if ((L::LOGMASK >> r) & 1u) {
       const double lv = log10(cur);
-      nv = pow(10.0, lv + wr * g);
+      nv = exp10(lv + wr * g);   // 10**lognew (apf_step2.py:69)
     } else {
       nv = cur + wr * g;
     }
@@ -201,10 +206,16 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     } else {
       C2p = ld_coef(st + WS::OC2);
     }
-    const ModelDesc<NSRC> md = make_model<NSRC>(q, C1p, C2p, A.bkgd_mode);
+    // the step's model descriptor goes to LDS: the sweep loads each field where it
+    // is used instead of holding 6*G doubles in registers across it
+    {
+      const ModelDesc<NSRC> md = make_model<NSRC>(q, C1p, C2p, A.bkgd_mode);
+      if (lane == 0) *mdl = md;
+    }
+    wave_sync();
 
     // build_analytical_model + chi_squared (:314-316)
-    const double part = sweep<NSRC, NT, false>(md, DE, vtab, nullptr, n, lane, A.fast != 0);
+    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane);
     const double chi = wave_sum(part);
 
     // accept_reject (:139-148)
@@ -282,10 +293,11 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n
   const Coef C2 = make_coef(p[L::S2X], p[L::S2Y], T2);
   auto q = [&](int k) -> double { return p[k]; };
   const ModelDesc<NSRC> md = make_model<NSRC>(q, C1, C2, bkgd_mode);
-  if constexpr (WRITE) {
-    sweep<NSRC, 0, true>(md, DE, vtab, out + (size_t)w * n * n, n, lane, fast != 0);
-  } else {
-    const double chi = wave_sum(sweep<NSRC, 0, false>(md, DE, vtab, nullptr, n, lane, fast != 0));
+  double *o = WRITE ? out + (size_t)w * n * n : nullptr;
+  const double part = fast ? sweep<NSRC, 0, WRITE, true>(md, DE, vtab, o, n, lane)
+                           : sweep<NSRC, 0, WRITE, false>(md, DE, vtab, o, n, lane);
+  if constexpr (!WRITE) {
+    const double chi = wave_sum(part);
     if (lane == 0) out[w] = chi;
   }
 }
@@ -394,10 +406,10 @@ size_t lds_bytes(const olpe_ctx *c, int wpb) {
   return b;
 }
 
-template <int NSRC, int NT, bool LDS, int WPB>
+template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   const size_t shm = lds_bytes(c, WPB);
-  auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB>;
+  auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB, FAST>;
   static bool attr_set = false;
   if (!attr_set) {
     HIPCHK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -410,20 +422,25 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   return OLPE_OK;
 }
 
-template <int NSRC> int launch_gibbs_n(olpe_ctx *c, const GibbsArgs &a) {
+template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &a) {
   if (c->lds_img) {
     switch (c->n) {
-      case 32: return launch_gibbs_t<NSRC, 32, true, 16>(c, a);
-      case 64: return launch_gibbs_t<NSRC, 64, true, 16>(c, a);
-      default: return launch_gibbs_t<NSRC, 0, true, 16>(c, a);
+      case 32: return launch_gibbs_t<NSRC, 32, true, 16, FAST>(c, a);
+      case 64:
+        if (c->wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
+        if (c->wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
+        return launch_gibbs_t<NSRC, 64, true, 16, FAST>(c, a);
+      default: return launch_gibbs_t<NSRC, 0, true, 16, FAST>(c, a);
     }
   }
-  if (c->n == 128) return launch_gibbs_t<NSRC, 128, false, 4>(c, a);
-  return launch_gibbs_t<NSRC, 0, false, 4>(c, a);
+  if (c->n == 128) return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
+  return launch_gibbs_t<NSRC, 0, false, 4, FAST>(c, a);
 }
 
 int launch_gibbs(olpe_ctx *c, const GibbsArgs &a) {
-  return c->nsrc == 2 ? launch_gibbs_n<2>(c, a) : launch_gibbs_n<3>(c, a);
+  const bool fast = c->eval_mode == OLPE_EVAL_FAST;
+  if (c->nsrc == 2) return fast ? launch_gibbs_m<2, true>(c, a) : launch_gibbs_m<2, false>(c, a);
+  return fast ? launch_gibbs_m<3, true>(c, a) : launch_gibbs_m<3, false>(c, a);
 }
 
 int ensure_ensemble(olpe_ctx *c, int W) {
@@ -498,6 +515,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
   c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) <= 160 * 1024;
+  if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
   std::vector<double2> hDE(npix);
   for (size_t i = 0; i < npix; ++i) {
@@ -706,7 +724,6 @@ int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_strid
 
   GibbsArgs a;
   a.DE = c->d_DE;
-  a.fast = c->eval_mode == OLPE_EVAL_FAST;
   a.n = c->n;
   a.bkgd_mode = c->bkgd_mode;
   a.W = c->W;

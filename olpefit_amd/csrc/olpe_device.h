@@ -196,7 +196,8 @@ struct Gauss {
 };
 
 __device__ __forceinline__ Trig make_trig(double th) {
-  const double c = cos(th), s = sin(th);
+  double s, c;
+  sincos(th, &s, &c);          // np.sin(theta), np.cos(theta): one range reduction
   return Trig{c * c, s * s, sin(2. * th)};
 }
 
@@ -258,7 +259,7 @@ struct ColWalk {
 //   q = ((a*dx^2) + ((b*dx)*dy)) + (c*dy^2);  v = A*exp(-q)
 //   model = ((wide_0 + narrow_0) + (wide_1 + narrow_1) [+ ...]) + bg
 //   t = (D - model) * invE;  acc += t*t
-template <int NSRC, int NT, bool WRITE>
+template <int NSRC, int NT, bool WRITE, int UNROLL = 2>
 __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const double2 *DE,
                                               double *out, int n_rt, int lane) {
   constexpr int G = 2 * NSRC;
@@ -277,7 +278,7 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
       t2[g] = m.g[g].k.b * xd;
     }
     const int jj = act ? j : 0;
-#pragma unroll 2
+#pragma unroll UNROLL
     for (int i = cw.grp; i < n; i += cw.S) {
       const double yi = (double)i;
       double v[G];
@@ -362,6 +363,8 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
       U[g] = exp(-(m.g[g].k.a * (xd * xd)));
       E[g] = exp(-(bx * S));
       Wc[g] = exp(-(bx * (y0r - m.g[g].y0)));
+      // one Gaussian's three exps at a time: caps the registers of this setup phase
+      __builtin_amdgcn_sched_barrier(0);
     }
     const int jj = act ? j : 0;
 #pragma unroll 2
@@ -393,13 +396,18 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
   return acc;
 }
 
-template <int NSRC, int NT, bool WRITE>
+// FAST kernels keep the exact sweep only as the (rare) fallback, unrolled once so
+// that it does not set the kernel's register budget.
+template <int NSRC, int NT, bool WRITE, bool FAST>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *DE,
-                                        double *vtab, double *out, int n, int lane,
-                                        bool fast) {
-  if (fast && fast_ok<NSRC>(m, NT ? NT : n))
-    return sweep_fast<NSRC, NT, WRITE>(m, DE, vtab, out, n, lane);
-  return sweep_exact<NSRC, NT, WRITE>(m, DE, out, n, lane);
+                                        double *vtab, double *out, int n, int lane) {
+  if constexpr (FAST) {
+    if (fast_ok<NSRC>(m, NT ? NT : n))
+      return sweep_fast<NSRC, NT, WRITE>(m, DE, vtab, out, n, lane);
+    return sweep_exact<NSRC, NT, WRITE, 1>(m, DE, out, n, lane);
+  } else {
+    return sweep_exact<NSRC, NT, WRITE, 2>(m, DE, out, n, lane);
+  }
 }
 
 }  // namespace olpe

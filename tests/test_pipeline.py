@@ -1,0 +1,127 @@
+"""Host-side file surface (CPU): CSV / acceptance bytes vs the reference's own writer
+output (golden *_csv written by apf_step2.py:355-365 under make_golden.py), FITS I/O vs
+astropy-written files, path/guess/initial-vector logic, and the step-3 read contract."""
+import os
+
+import numpy as np
+import pytest
+
+from olpefit_amd import fitsio, pipeline, step3, synth
+from oracle import olpe_oracle as ora
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ["c32", "c64", "c64_3", "c128_3"]
+
+
+def _rows_and_counters(g, w):
+    """Reference file content after the last write (count = last multiple of 10)."""
+    L = int(g["traj_len"][w])
+    last = (L // 10) * 10
+    burn = int(g["burn_in"])
+    first = max(burn, 1)
+    rows = g["traj_params"][w, first - 1:last]
+    npar = rows.shape[1] - 1
+    tries = np.zeros(npar)
+    acc = np.zeros(npar)
+    for i in range(last):
+        r = g["traj_r"][w, i]
+        tries[r] += 1
+        acc[r] += g["traj_acc"][w, i]
+    return rows, tries, acc
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_chain_csv_bytes_match_reference_writer(golden, name):
+    g = golden(name)
+    rows, _, _ = _rows_and_counters(g, 0)
+    text = pipeline.format_rows(pipeline.with_seed_row(rows))
+    with open(os.path.join(GOLDEN, f"{name}_csv", "0_finalarray_mpi.csv"), newline="") as f:
+        ref = f.read()
+    assert text == ref
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_acceptance_text_matches_reference(golden, name):
+    g = golden(name)
+    for w in range(len(g["seeds"])):
+        _, tries, acc = _rows_and_counters(g, w)
+        with open(os.path.join(GOLDEN, f"{name}_csv", f"{w}_acceptance_rate.csv")) as f:
+            assert pipeline.acceptance_text(acc, tries) == f.read()
+
+
+def test_written_rows_rule():
+    assert pipeline.written_rows(847, 5) == 836          # rows for counts 5..840
+    assert pipeline.written_rows(237, 0) == 230          # counts 1..230
+    assert pipeline.written_rows(9, 0) == 0
+    assert pipeline.written_rows(6000, 6000) == 1
+
+
+def test_fits_reader_matches_astropy_files():
+    exp = np.load(os.path.join(GOLDEN, "fits_expected.npz"))
+    d, h = fitsio.getdata_header(os.path.join(GOLDEN, "astropy_f32.fits"))
+    assert d.dtype == np.dtype(">f4") and np.array_equal(d, exp["f32"])
+    assert h["itime"] == 1.0 and h["COADDS"] == 1 and h["sampmode"] == 2
+    assert h["OBJECT"] == "synthetic"
+    d, h = fitsio.getdata_header(os.path.join(GOLDEN, "astropy_u16.fits"))
+    assert np.array_equal(d, exp["u16"]) and h["SAMPMODE"] == 3
+    d, _ = fitsio.getdata_header(os.path.join(GOLDEN, "astropy_f64.fits"))
+    assert np.array_equal(d, exp["f64"])
+
+
+def test_fits_roundtrip(tmp_path):
+    img, _ = synth.make_image(32, 2, 0)
+    p = str(tmp_path / "x.fits")
+    fitsio.write(p, img, synth.HEADER)
+    d, h = fitsio.getdata_header(p)
+    assert np.array_equal(d, img) and h["multisam"] == 1
+    assert os.path.getsize(p) % 2880 == 0
+
+
+def test_paths_and_guess(tmp_path):
+    path = synth.write_case(str(tmp_path), 32, 2)
+    directory, frame, out = pipeline.image_paths(path)
+    assert frame == "00001" and out == directory + "00001_apf_results/"
+    g = pipeline.read_guess(directory + "00001_initialguess")
+    assert np.allclose(g, synth.guess_values(32, 2))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_initial_parameters_match_reference(golden, name):
+    g = golden(name)
+    p = pipeline.initial_parameters(g["image"], g["guess"], int(g["nsrc"]))
+    assert np.array_equal(p[:-1], g["p_init"][:-1])
+    assert np.array_equal(p, ora.initial_parameters(g["image"], g["guess"], int(g["nsrc"])))
+
+
+def test_noise_model_matches_oracle(golden):
+    from olpefit_amd.core import noise_model
+    g = golden("c64")
+    mask, pois2, rn2, sat, rn = noise_model(g["image"], 1.0, 1, 1, 2)
+    assert np.array_equal(mask, g["mask"])
+    err = np.sqrt(rn2 + pois2.astype(np.float64))
+    assert np.array_equal(err, g["err"])
+
+
+def test_step3_reader_and_gelman_rubin(tmp_path, golden):
+    """Write chains with the build's writer, read them back with the step-3 contract
+    (equal lengths, NaN row dropped by additional_burnin=1) and compare GR with the
+    oracle's restatement of apf_step3.py:260-278."""
+    rs = np.random.RandomState(3)
+    chains = rs.normal(size=(4, 50, 17))
+    for w in range(4):
+        pipeline.write_chain_csv(str(tmp_path / f"{w}_finalarray_mpi.csv"),
+                                 pipeline.with_seed_row(chains[w]))
+    c = step3.load_chains(str(tmp_path), 4, additional_burnin=1)
+    assert c.shape == (50, 4, 17)
+    assert np.array_equal(c[:, 2, :], chains[2])
+    for k in range(16):
+        ps1, rc1 = step3.gelman_rubin(c[:, :, k])
+        ps2, rc2 = ora.gelman_rubin(c[:, :, k])
+        assert ps1 == ps2 and rc1 == rc2
+    s = step3.summary(c)
+    assert set(s) == set(step3.NAMES_2[:-1])
+    # unequal lengths are an error, as in the reference's [length, ncor] assignment
+    pipeline.write_chain_csv(str(tmp_path / "3_finalarray_mpi.csv"),
+                             pipeline.with_seed_row(chains[3][:10]))
+    with pytest.raises(ValueError):
+        step3.load_chains(str(tmp_path), 4)
