@@ -133,29 +133,10 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import datetime
-
-        import torch
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo", rank=rank, world_size=world,
-                                 timeout=datetime.timedelta(minutes=10))
-        dist = tdist
-
-    def barrier():
-        if dist:
-            dist.barrier()
-
-    def allmax(x: float) -> float:
-        if not dist:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    from olpefit_amd import dist as odist
+    rank, world, local = odist.env()
+    group = odist.HostGroup(rank, world)
+    barrier, allmax = group.barrier, group.allmax
 
     from olpefit_amd import synth
     from olpefit_amd.core import Sampler
@@ -169,8 +150,7 @@ def main():
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
     p0[-1] = s.chi_squared(p0)
-    seeds = 1000 + rank * wpg + np.arange(wpg)
-    s.seed(seeds)
+    s.seed(odist.walker_seeds(1000, rank * wpg, wpg))      # weak scaling: wpg per GPU
     s.set_state(np.tile(p0, (wpg, 1)))
 
     def measure(mode, steps, warmup):
@@ -200,11 +180,9 @@ def main():
 
     # end-of-run exchange: RCCL all-gather of final walker states
     gather_ms = None
-    if dist:
-        import torch
-        uid = [Sampler.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        s.comm_init(uid[0], world, rank)
+    if world > 1:
+        uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
+        s.comm_init(uid, world, rank)
         barrier()
         tg = time.perf_counter()
         allst = s.allgather_state()
@@ -213,8 +191,7 @@ def main():
 
     if rank != 0:
         s.close()
-        if dist:
-            dist.destroy_process_group()
+        group.close()
         return
 
     total = world * wpg * args.iters * args.steps
@@ -274,8 +251,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(n, nsrc, args.cpu_iters, procs)
     print(json.dumps(out))
     s.close()
-    if dist:
-        dist.destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

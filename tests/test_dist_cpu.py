@@ -1,0 +1,83 @@
+"""The N>1 path on CPU: two gloo ranks run the host orchestration of bench.py /
+olpefit_amd.dist (shard ranges, global-index seeds, barrier, max-over-ranks timing,
+id broadcast) with the oracle standing in for the per-GPU sampler, and the gathered
+per-rank chains equal a single-process run of all walkers (chains do not depend on
+the number of GPUs)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from olpefit_amd import dist as odist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_chains(seeds, n_iters):
+    from olpefit_amd import synth
+    from oracle import olpe_oracle as ora
+    img, _ = synth.make_image(32, 2, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = ora.initial_parameters(img, synth.guess_values(32, 2), 2)
+    out = []
+    for sd in seeds:
+        w = ora.Walker(dm, err, p0, int(sd))
+        w.init_chi2()
+        out.append(w.run(n_iters)[0])
+    return np.array(out)
+
+
+def _rank_main(rank, world, port, total, n_iters, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    r, w, _ = odist.env()
+    g = odist.HostGroup(r, w)
+    w0, n = odist.shard(total, w, r)
+    seeds = odist.walker_seeds(1000, w0, n)
+    uid = g.broadcast(b"x" * 128 if r == 0 else None)
+    g.barrier()
+    chains = _oracle_chains(seeds, n_iters)
+    t = g.allmax(float(r + 1))
+    gathered = [None] * w
+    dist.all_gather_object(gathered, (w0, chains))
+    if r == 0:
+        q.put((uid, t, gathered))
+    g.close()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_two_rank_gloo_sharding_matches_single_process(world):
+    total, n_iters = 5, 60
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, total, n_iters, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    uid, tmax, gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert uid == b"x" * 128 and tmax == float(world)
+    got = np.concatenate([c for _, c in sorted(gathered, key=lambda x: x[0])], axis=0)
+    ref = _oracle_chains(odist.walker_seeds(1000, 0, total), n_iters)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_shard_and_seed_helpers():
+    assert [odist.shard(10, 3, r) for r in range(3)] == [(0, 3), (3, 3), (6, 4)]
+    assert sum(odist.shard(524288, 8, r)[1] for r in range(8)) == 524288
+    s = odist.walker_seeds(2 ** 32 - 2, 0, 4)
+    assert list(s) == [2 ** 32 - 2, 2 ** 32 - 1, 0, 1]
+    g = odist.HostGroup(0, 1)
+    assert g.allmax(3.5) == 3.5 and g.broadcast("a") == "a"

@@ -235,3 +235,22 @@ def test_errors_are_reported(golden, lib_loaded):
     s = make_sampler(golden("c32"))
     with pytest.raises(OlpeError):
         s.run(10)                                        # not seeded
+
+
+def test_rccl_single_rank_collectives(golden, lib_loaded):
+    """RCCL communicator with one rank on the box's GPU: the all-gather returns the
+    walker states and the all-reduced moments equal NumPy's over the last chain."""
+    from olpefit_amd.core import Sampler
+    g = golden("c32")
+    s = make_sampler(g)
+    s.seed(np.arange(50, 58))
+    s.set_state(np.tile(g["p_init"], (8, 1)))
+    chain = s.run(40, burn_in=0, record_stride=4)
+    s.comm_init(Sampler.comm_unique_id(), 1, 0)
+    st, _, _ = s.get_state()
+    np.testing.assert_array_equal(s.allgather_state(), st)
+    m = s.allreduce_moments()
+    flat = chain.reshape(-1, s.ps)
+    assert m[0] == flat.shape[0]
+    np.testing.assert_allclose(m[1:1 + s.ps], flat.sum(axis=0), rtol=1e-12)
+    np.testing.assert_allclose(m[1 + s.ps:], (flat ** 2).sum(axis=0), rtol=1e-12)

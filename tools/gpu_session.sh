@@ -1,14 +1,17 @@
 #!/bin/bash
-# One GPU session: parity tests, bench (exact + fast), rocprofv3 kernel stats, PMC traffic.
-# usage: tools/gpu_session.sh <round-tag>
+# One GPU session: parity tests, bench, rocprofv3 kernel stats, PMC traffic passes.
+# usage: tools/gpu_session.sh <round-tag> [skip-tests]
 tag=${1:-r01}
 export TMPDIR=/tmp
-B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+B="python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-alt"
+T="gpu_tests:900:python -m pytest tests -q -m gpu -rf"
+[ "$2" = "skip-tests" ] && T="noop:10:true"
 tools/gpu_steps.sh \
-  "gpu_tests:900:python -m pytest tests -q -m gpu -rf" \
-  "bench_exact:300:python bench.py --mode exact" \
-  "bench_fast:300:python bench.py --mode fast" \
-  "prof_exact:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_exact -o run --output-format csv -- $B --mode exact" \
+  "$T" \
+  "bench:400:python bench.py" \
   "prof_fast:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_fast -o run --output-format csv -- $B --mode fast" \
+  "prof_exact:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_exact -o run --output-format csv -- $B --mode exact" \
   "pmc_fetch_fast:300:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${tag}_fetch_fast -o run --output-format csv -- $B --mode fast" \
-  "pmc_write_fast:300:rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${tag}_write_fast -o run --output-format csv -- $B --mode fast"
+  "pmc_write_fast:300:rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${tag}_write_fast -o run --output-format csv -- $B --mode fast" \
+  "pmc_fetch_exact:300:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${tag}_fetch_exact -o run --output-format csv -- $B --mode exact" \
+  "pmc_write_exact:300:rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${tag}_write_exact -o run --output-format csv -- $B --mode exact"
