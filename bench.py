@@ -54,12 +54,13 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
 
     exact: per pixel-Gaussian 7 ops + one exp, per pixel G-1 combines + background +
            3 residual ops, per column-Gaussian 4 hoisted ops.
-    fast:  per pixel-Gaussian 3 multiplies (+1 combine), per pixel 3 residual ops,
-           per Gaussian 4 exps per row/column (U, E, W0, V) with ~4 ops each."""
+    fast:  per pixel-Gaussian 2 multiplies + 1 combine, per pixel 2 fma (residual and
+           accumulate); per Gaussian and column 2 exps + 6 ops, per Gaussian and row
+           1 exp + 3 ops."""
     g = 2 * nsrc
     if mode == "exact":
         return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
-    return n * n * (4 * g + 3) + 4 * n * g * (EXP_OPS + 4)
+    return n * n * (3 * g + 2) + n * g * (3 * EXP_OPS + 9)
 
 
 def sec8d_work(n: int, nsrc: int) -> float:

@@ -43,7 +43,7 @@ template <int NSRC> __device__ __forceinline__ double width_of(int r) {
 }
 
 struct GibbsArgs {
-  const double2 *DE;   // [n*n] {data, 1/err} ({0,0} where masked)
+  const double2 *DE;   // [n*n] {data, 1/err} (EXACT) or {data/err, 1/err} (FAST); {0,0} masked
   int n;
   int bkgd_mode;
   long long W;
@@ -517,17 +517,20 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) <= 160 * 1024;
   if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
-  std::vector<double2> hDE(npix);
+  std::vector<double2> hDE(npix), hDW(npix);
   for (size_t i = 0; i < npix; ++i) {
     const double d = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)image)[i]
                                                    : ((const double *)image)[i];
     const double p2 = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)pois2)[i]
                                                     : ((const double *)pois2)[i];
     const double e = sqrt(readnoise2 + p2);   // apf_step2.py:210
-    if (mask && mask[i])
+    if (mask && mask[i]) {
       hDE[i] = make_double2(0.0, 0.0);
-    else
+      hDW[i] = make_double2(0.0, 0.0);
+    } else {
       hDE[i] = make_double2(d, 1.0 / e);
+      hDW[i] = make_double2(d * (1.0 / e), 1.0 / e);
+    }
   }
   int rc;
   hipError_t e1 = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -537,11 +540,13 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   }
   (void)hipEventCreate(&c->ev0);
   (void)hipEventCreate(&c->ev1);
-  if ((rc = dev_alloc(&c->d_DE, npix))) {
+  if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix))) {
     olpe_destroy(c);
     return rc;
   }
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
+  if (e2 == hipSuccess)
+    e2 = hipMemcpy(c->d_DW, hDW.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 != hipSuccess) {
     olpe_destroy(c);
     return set_err(OLPE_EHIP, "hipMemcpy image: %s", hipGetErrorString(e2));
@@ -555,7 +560,7 @@ void olpe_destroy(olpe_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   olpe_comm_release(c);
-  void *ptrs[] = {c->d_DE, c->d_state, c->d_tries, c->d_acc,
+  void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2};
   for (void *p : ptrs)
@@ -593,17 +598,17 @@ static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, boo
   if (shm > 65536) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
   if (c->nsrc == 2) {
     if (write)
-      hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, shm, c->stream, c->d_DE,
+      hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, shm, c->stream, fast ? c->d_DW : c->d_DE,
                          c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
     else
-      hipLaunchKernelGGL((olpe_eval_kernel<2, false>), grid, block, shm, c->stream, c->d_DE,
+      hipLaunchKernelGGL((olpe_eval_kernel<2, false>), grid, block, shm, c->stream, fast ? c->d_DW : c->d_DE,
                          c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
   } else {
     if (write)
-      hipLaunchKernelGGL((olpe_eval_kernel<3, true>), grid, block, shm, c->stream, c->d_DE,
+      hipLaunchKernelGGL((olpe_eval_kernel<3, true>), grid, block, shm, c->stream, fast ? c->d_DW : c->d_DE,
                          c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
     else
-      hipLaunchKernelGGL((olpe_eval_kernel<3, false>), grid, block, shm, c->stream, c->d_DE,
+      hipLaunchKernelGGL((olpe_eval_kernel<3, false>), grid, block, shm, c->stream, fast ? c->d_DW : c->d_DE,
                          c->n, c->bkgd_mode, fast, c->d_scratch, W, c->d_scratch2);
   }
   HIPCHK(hipGetLastError());
@@ -723,7 +728,7 @@ int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_strid
   c->trace_iters = c->trace_on ? n_iters : 0;
 
   GibbsArgs a;
-  a.DE = c->d_DE;
+  a.DE = c->eval_mode == OLPE_EVAL_FAST ? c->d_DW : c->d_DE;
   a.n = c->n;
   a.bkgd_mode = c->bkgd_mode;
   a.W = c->W;

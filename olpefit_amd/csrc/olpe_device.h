@@ -304,15 +304,58 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
   return acc;
 }
 
+// Exact per-pixel model with the fast kernels' {D/err, 1/err} image: the fallback of
+// FAST kernels for steps that fail the fast_ok guard (residual in the fma form).
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep_exact_dw(const ModelDesc<NSRC> &m, const double2 *DW,
+                                                 double *out, int n_rt, int lane) {
+  constexpr int G = 2 * NSRC;
+  const int n = NT ? NT : n_rt;
+  const ColWalk cw(n, lane);
+  double acc = 0.0;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int j = c0 + cw.jl;
+    const bool act = cw.lane_ok && j < n;
+    const double xj = (double)j;
+    const int jj = act ? j : 0;
+#pragma unroll 1
+    for (int i = cw.grp; i < n; i += cw.S) {
+      const double yi = (double)i;
+      double v[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const double xd = xj - m.g[g].x0;
+        const double yd = yi - m.g[g].y0;
+        const double qq = (m.g[g].k.a * (xd * xd) + (m.g[g].k.b * xd) * yd) +
+                          m.g[g].k.c * (yd * yd);
+        v[g] = m.g[g].amp * exp(-qq);
+      }
+      double mod = v[0] + v[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
+      mod = mod + m.bg;
+      if constexpr (WRITE) {
+        if (act) out[i * n + j] = mod;
+      } else {
+        const double2 dw = DW[i * n + jj];
+        const double t = fma(-mod, dw.y, dw.x);
+        acc = act ? fma(t, t, acc) : acc;
+      }
+    }
+  }
+  return acc;
+}
+
 // FAST evaluation: with dx = j - x0, dy = i - y0,
-//   A*exp(-(a dx^2 + b dx dy + c dy^2)) = (U_j * V_i) * W_ij
-//   U_j = exp(-a dx^2)            one exp per lane (column), per step
-//   V_i = A * exp(-c dy^2)        one exp per lane (row), per step, kept in LDS
-//   W_ij = exp(-b dx dy)          W_(i+S) = W_ij * exp(-b dx S): one multiply
-// so a pixel-Gaussian costs 3 multiplies instead of an exp.  Valid while the cross
-// term stays bounded (|b dx dy| < kFastCross over the grid): then U*V can only
-// underflow where the Gaussian is < e^-400 anyway.  Otherwise (or for non-finite
-// parameters) the exact sweep runs -- a wave-uniform decision.
+//   A*exp(-(a dx^2 + b dx dy + c dy^2)) = V_i * W_ij
+//   V_i  = exp(-c dy^2)                      one exp per lane (row), kept in LDS
+//   W_ij = A*exp(-(a dx^2 + b dx dy))        one exp per lane (column) at the first row,
+//          W_(i+S)j = W_ij * E_j,  E_j = exp(-b dx S)   one more exp per column
+// so a pixel-Gaussian costs 2 multiplies instead of an exp.  The image is staged as
+// DW[pixel] = {D/err, 1/err} so the residual is one fma: t = D/err - M*(1/err).
+// Valid while the cross term stays bounded (|b dx dy| < kFastCross over the grid):
+// then W can only underflow where the Gaussian is < e^-400.  Otherwise (or for
+// non-finite parameters) the exact sweep runs -- a wave-uniform decision.
 constexpr double kFastCross = 300.0;
 
 template <int NSRC>
@@ -332,19 +375,19 @@ __device__ __forceinline__ bool fast_ok(const ModelDesc<NSRC> &m, int n) {
 }
 
 template <int NSRC, int NT, bool WRITE>
-__device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const double2 *DE,
+__device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const double2 *DW,
                                              double *vtab, double *out, int n_rt,
                                              int lane) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
   const ColWalk cw(n, lane);
-  // row table V[i][g] = A_g * exp(-c_g dy^2), rows lane-parallel
+  // row table V[i][g] = exp(-c_g dy^2), rows lane-parallel
   for (int i = lane; i < n; i += 64) {
     const double yi = (double)i;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const double yd = yi - m.g[g].y0;
-      vtab[i * G + g] = m.g[g].amp * exp(-(m.g[g].k.c * (yd * yd)));
+      vtab[i * G + g] = exp(-(m.g[g].k.c * (yd * yd)));
     }
   }
   wave_sync();
@@ -355,15 +398,14 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
     const int j = c0 + cw.jl;
     const bool act = cw.lane_ok && j < n;
     const double xj = (double)j;
-    double U[G], E[G], Wc[G];
+    double E[G], Wc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const double xd = xj - m.g[g].x0;
       const double bx = m.g[g].k.b * xd;
-      U[g] = exp(-(m.g[g].k.a * (xd * xd)));
+      Wc[g] = m.g[g].amp * exp(-(m.g[g].k.a * (xd * xd) + bx * (y0r - m.g[g].y0)));
       E[g] = exp(-(bx * S));
-      Wc[g] = exp(-(bx * (y0r - m.g[g].y0)));
-      // one Gaussian's three exps at a time: caps the registers of this setup phase
+      // one Gaussian's exps at a time: caps the registers of this setup phase
       __builtin_amdgcn_sched_barrier(0);
     }
     const int jj = act ? j : 0;
@@ -374,8 +416,8 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
 #pragma unroll
       for (int h = 0; h < G / 2; ++h) {
         const double2 vv = vr[h];
-        v[2 * h] = (U[2 * h] * vv.x) * Wc[2 * h];
-        v[2 * h + 1] = (U[2 * h + 1] * vv.y) * Wc[2 * h + 1];
+        v[2 * h] = vv.x * Wc[2 * h];
+        v[2 * h + 1] = vv.y * Wc[2 * h + 1];
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) Wc[g] = Wc[g] * E[g];
@@ -386,8 +428,8 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
       if constexpr (WRITE) {
         if (act) out[i * n + j] = mod;
       } else {
-        const double2 de = DE[i * n + jj];
-        const double t = (de.x - mod) * de.y;
+        const double2 dw = DW[i * n + jj];
+        const double t = fma(-mod, dw.y, dw.x);
         acc = act ? fma(t, t, acc) : acc;
       }
     }
@@ -399,14 +441,15 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
 // FAST kernels keep the exact sweep only as the (rare) fallback, unrolled once so
 // that it does not set the kernel's register budget.
 template <int NSRC, int NT, bool WRITE, bool FAST>
-__device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *DE,
+__device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane) {
+  // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
   if constexpr (FAST) {
     if (fast_ok<NSRC>(m, NT ? NT : n))
-      return sweep_fast<NSRC, NT, WRITE>(m, DE, vtab, out, n, lane);
-    return sweep_exact<NSRC, NT, WRITE, 1>(m, DE, out, n, lane);
+      return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+    return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
   } else {
-    return sweep_exact<NSRC, NT, WRITE, 2>(m, DE, out, n, lane);
+    return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
   }
 }
 

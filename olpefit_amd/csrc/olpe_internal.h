@@ -16,7 +16,8 @@ struct olpe_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
-  double2 *d_DE = nullptr;   // [n*n] {data as f64, 1/err}, {0,0} where masked
+  double2 *d_DE = nullptr;   // [n*n] {data as f64, 1/err}, {0,0} where masked (EXACT)
+  double2 *d_DW = nullptr;   // [n*n] {data/err, 1/err}, {0,0} where masked (FAST)
   // walker ensemble
   int W = 0;
   bool seeded = false;
