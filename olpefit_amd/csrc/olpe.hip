@@ -77,10 +77,10 @@ template <int NP> struct WaveSlice {
   static constexpr int U32 = MT_N + 2 * NP;                  // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
   static constexpr int NSRC = NP == 16 ? 2 : 3;
-  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
-  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
-  static constexpr int OPT = PS + 12, OPC = PS + 15;
-  static constexpr int F64 = PS + 18;
+  // doubles: params[PS] | T1[3] T2[3] | C1[4] C2[4] | pending T[3] C[4]
+  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 10;
+  static constexpr int OPT = PS + 14, OPC = PS + 17;
+  static constexpr int F64 = PS + 21;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
   static constexpr int BYTES = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
 };
@@ -89,12 +89,12 @@ __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsr
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
-__device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }
+__device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2], s[3]}; }
 __device__ __forceinline__ void st_trig(double *s, const Trig &t) {
   s[0] = t.cost2; s[1] = t.sint2; s[2] = t.sin2t;
 }
 __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
-  s[0] = k.a; s[1] = k.b; s[2] = k.c;
+  s[0] = k.a; s[1] = k.b; s[2] = k.c; s[3] = k.K;
 }
 
 template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
@@ -105,6 +105,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = NT ? NT : A.n;
   const int npix = n * n;
+  const double RS = (double)row_stride(n);
   const int lane = threadIdx.x & 63;
   // wave index as a provably uniform (SGPR) value: LDS slice addresses stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -143,8 +144,8 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     const Trig t1 = make_trig(st[L::T1]), t2 = make_trig(st[L::T2]);
     st_trig(st + WS::OT1, t1);
     st_trig(st + WS::OT2, t2);
-    st_coef(st + WS::OC1, make_coef(st[L::S1X], st[L::S1Y], t1));
-    st_coef(st + WS::OC2, make_coef(st[L::S2X], st[L::S2Y], t2));
+    st_coef(st + WS::OC1, make_coef(st[L::S1X], st[L::S1Y], t1, RS));
+    st_coef(st + WS::OC2, make_coef(st[L::S2X], st[L::S2Y], t2, RS));
   }
   wave_sync();
 
@@ -194,14 +195,14 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     Coef C1p, C2p;
     if (grp == 1) {
       const Trig t = (r == L::T1) ? make_trig(nv) : ld_trig(st + WS::OT1);
-      C1p = make_coef(q(L::S1X), q(L::S1Y), t);
+      C1p = make_coef(q(L::S1X), q(L::S1Y), t, RS);
       if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
     } else {
       C1p = ld_coef(st + WS::OC1);
     }
     if (grp == 2) {
       const Trig t = (r == L::T2) ? make_trig(nv) : ld_trig(st + WS::OT2);
-      C2p = make_coef(q(L::S2X), q(L::S2Y), t);
+      C2p = make_coef(q(L::S2X), q(L::S2Y), t, RS);
       if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
     } else {
       C2p = ld_coef(st + WS::OC2);
@@ -230,7 +231,8 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       if (grp) {
         double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
         double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
-        for (int k = 0; k < 3; ++k) { dt[k] = st[WS::OPT + k]; dc[k] = st[WS::OPC + k]; }
+        for (int k = 0; k < 3; ++k) dt[k] = st[WS::OPT + k];
+        for (int k = 0; k < 4; ++k) dc[k] = st[WS::OPC + k];
       }
     }
     wave_sync();
@@ -289,8 +291,9 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n
 #pragma unroll
   for (int k = 0; k < PS; ++k) p[k] = uniform_f64(params[w * PS + k]);
   const Trig T1 = make_trig(p[L::T1]), T2 = make_trig(p[L::T2]);
-  const Coef C1 = make_coef(p[L::S1X], p[L::S1Y], T1);
-  const Coef C2 = make_coef(p[L::S2X], p[L::S2Y], T2);
+  const double RS = (double)row_stride(n);
+  const Coef C1 = make_coef(p[L::S1X], p[L::S1Y], T1, RS);
+  const Coef C2 = make_coef(p[L::S2X], p[L::S2Y], T2, RS);
   auto q = [&](int k) -> double { return p[k]; };
   const ModelDesc<NSRC> md = make_model<NSRC>(q, C1, C2, bkgd_mode);
   double *o = WRITE ? out + (size_t)w * n * n : nullptr;

@@ -189,6 +189,7 @@ struct Trig {
 };
 struct Coef {
   double a, b, c;
+  double K;   // exp(-2 c S^2): row-step factor of sweep_fast2's second-order recurrence
 };
 struct Gauss {
   double amp, x0, y0;
@@ -201,12 +202,14 @@ __device__ __forceinline__ Trig make_trig(double th) {
   return Trig{c * c, s * s, sin(2. * th)};
 }
 
-__device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t) {
+__device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t,
+                                          double S = 1.0) {
   const double xstd2 = sx * sx, ystd2 = sy * sy;
   Coef k;
   k.a = 0.5 * ((t.cost2 / xstd2) + (t.sint2 / ystd2));
   k.b = 0.5 * ((t.sin2t / xstd2) - (t.sin2t / ystd2));
   k.c = 0.5 * ((t.sint2 / xstd2) + (t.cost2 / ystd2));
+  k.K = exp(-(2.0 * k.c * (S * S)));
   return k;
 }
 
@@ -243,6 +246,8 @@ __device__ __forceinline__ ModelDesc<NSRC> make_model(const Q &q, const Coef &C1
 // (n >= 64: j = 64*pass + L; n < 64: the wave covers 64/n row groups, stride S), so
 // per-column terms are computed once per step.
 // ---------------------------------------------------------------------------------
+__host__ __device__ constexpr int row_stride(int n) { return n >= 64 ? 1 : 64 / n; }
+
 struct ColWalk {
   int S, nc, grp, jl;
   bool lane_ok;
@@ -409,22 +414,119 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
       __builtin_amdgcn_sched_barrier(0);
     }
     const int jj = act ? j : 0;
+    const double bg = m.bg;
+    // software pipeline: the LDS rows (V table + pixel) of row i+S are read while
+    // row i is computed, so the LDS latency hides behind the multiplies
+    const double2 *vr = reinterpret_cast<const double2 *>(vtab) + cw.grp * (G / 2);
+    const int vstep = cw.S * (G / 2);
+    double2 vv[G / 2], dw;
+#pragma unroll
+    for (int h = 0; h < G / 2; ++h) vv[h] = vr[h];
+    dw = WRITE ? make_double2(0.0, 0.0) : DW[cw.grp * n + jj];
 #pragma unroll 2
     for (int i = cw.grp; i < n; i += cw.S) {
-      const double2 *vr = reinterpret_cast<const double2 *>(vtab + i * G);
+      const bool more = i + cw.S < n;
+      double2 nv[G / 2], ndw;
+      const double2 *nr = vr + (more ? vstep : 0);
+#pragma unroll
+      for (int h = 0; h < G / 2; ++h) nv[h] = nr[h];
+      if constexpr (!WRITE) ndw = DW[(more ? i + cw.S : i) * n + jj];
       double v[G];
 #pragma unroll
       for (int h = 0; h < G / 2; ++h) {
-        const double2 vv = vr[h];
-        v[2 * h] = vv.x * Wc[2 * h];
-        v[2 * h + 1] = vv.y * Wc[2 * h + 1];
+        v[2 * h] = vv[h].x * Wc[2 * h];
+        v[2 * h + 1] = vv[h].y * Wc[2 * h + 1];
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) Wc[g] = Wc[g] * E[g];
       double mod = v[0] + v[1];
 #pragma unroll
       for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
-      mod = mod + m.bg;
+      mod = mod + bg;
+      if constexpr (WRITE) {
+        if (act) out[i * n + j] = mod;
+      } else {
+        const double t = fma(-mod, dw.y, dw.x);
+        acc = act ? fma(t, t, acc) : acc;
+        dw = ndw;
+      }
+#pragma unroll
+      for (int h = 0; h < G / 2; ++h) vv[h] = nv[h];
+      vr = nr;
+    }
+  }
+  wave_sync();   // vtab is rewritten by the next step
+  return acc;
+}
+
+// FAST2 evaluation: second-order recurrence down each column, no row table.
+// Q(i) = (a dx^2 + b dx dy_i) + c dy_i^2 is quadratic in the row i, so with stride S
+//   G_(i+S) = G_i * R_i,   R_(i+S) = R_i * K,   K = exp(-2 c S^2)
+// starting from G_i0 = A exp(-Q(i0)) and R_i0 = exp(-(Q(i0+S) - Q(i0))): two multiplies
+// per pixel-Gaussian and no LDS traffic besides the pixel itself.  Rounding grows
+// like m^2/2 ulp after m rows (<= 2048 ulp at 64 rows, typically ~300).  Guard: every
+// value of Q over the grid (max at a corner, Q is convex) stays below kFast2Q, so no
+// G underflows and |Q(i+S) - Q(i)| < kFast2Q keeps R finite.
+constexpr double kFast2Q = 690.0;
+
+template <int NSRC>
+__device__ __forceinline__ bool fast2_ok(const ModelDesc<NSRC> &m, int n) {
+  bool ok = true;
+  const double hi = (double)(n - 1);
+#pragma unroll
+  for (int g = 0; g < 2 * NSRC; ++g) {
+    const Gauss &q = m.g[g];
+    double qmax = 0.0;
+#pragma unroll
+    for (int cx = 0; cx < 2; ++cx)
+#pragma unroll
+      for (int cy = 0; cy < 2; ++cy) {
+        const double xd = (cx ? hi : 0.0) - q.x0, yd = (cy ? hi : 0.0) - q.y0;
+        qmax = fmax(qmax, (q.k.a * (xd * xd) + (q.k.b * xd) * yd) + q.k.c * (yd * yd));
+      }
+    ok = ok && (qmax < kFast2Q) && isfinite(q.amp) && isfinite(q.k.K);
+  }
+  return ok;
+}
+
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const double2 *DW,
+                                              double *out, int n_rt, int lane) {
+  constexpr int G = 2 * NSRC;
+  const int n = NT ? NT : n_rt;
+  const ColWalk cw(n, lane);
+  double acc = 0.0;
+  const double S = (double)cw.S;
+  const double yr = (double)cw.grp;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int j = c0 + cw.jl;
+    const bool act = cw.lane_ok && j < n;
+    const double xj = (double)j;
+    double Gv[G], R[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double xd = xj - m.g[g].x0;
+      const double yd = yr - m.g[g].y0;
+      const double bx = m.g[g].k.b * xd;
+      const double q0 = (m.g[g].k.a * (xd * xd) + bx * yd) + m.g[g].k.c * (yd * yd);
+      const double d1 = bx * S + (m.g[g].k.c * S) * (2.0 * yd + S);
+      Gv[g] = m.g[g].amp * exp(-q0);
+      R[g] = exp(-d1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int jj = act ? j : 0;
+    const double bg = m.bg;
+#pragma unroll 4
+    for (int i = cw.grp; i < n; i += cw.S) {
+      double mod = Gv[0] + Gv[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) mod = mod + (Gv[2 * s] + Gv[2 * s + 1]);
+      mod = mod + bg;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        Gv[g] = Gv[g] * R[g];
+        R[g] = R[g] * m.g[g].k.K;
+      }
       if constexpr (WRITE) {
         if (act) out[i * n + j] = mod;
       } else {
@@ -434,7 +536,6 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
       }
     }
   }
-  wave_sync();   // vtab is rewritten by the next step
   return acc;
 }
 
@@ -445,8 +546,11 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
                                         double *vtab, double *out, int n, int lane) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
   if constexpr (FAST) {
-    if (fast_ok<NSRC>(m, NT ? NT : n))
+    const int nn = NT ? NT : n;
+    if (fast_ok<NSRC>(m, nn)) {
+      if (fast2_ok<NSRC>(m, nn)) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
       return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+    }
     return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
   } else {
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
