@@ -310,7 +310,7 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
 }
 
 // Exact per-pixel model with the fast kernels' {D/err, 1/err} image: the fallback of
-// FAST kernels for steps that fail the fast_ok guard (residual in the fma form).
+// FAST kernels for steps that fail both fast guards (residual in the fma form).
 template <int NSRC, int NT, bool WRITE>
 __device__ __forceinline__ double sweep_exact_dw(const ModelDesc<NSRC> &m, const double2 *DW,
                                                  double *out, int n_rt, int lane) {
@@ -360,25 +360,8 @@ __device__ __forceinline__ double sweep_exact_dw(const ModelDesc<NSRC> &m, const
 // DW[pixel] = {D/err, 1/err} so the residual is one fma: t = D/err - M*(1/err).
 // Valid while the cross term stays bounded (|b dx dy| < kFastCross over the grid):
 // then W can only underflow where the Gaussian is < e^-400.  Otherwise (or for
-// non-finite parameters) the exact sweep runs -- a wave-uniform decision.
+// non-finite parameters) the exact sweep runs -- a wave-uniform decision (fast_level).
 constexpr double kFastCross = 300.0;
-
-template <int NSRC>
-__device__ __forceinline__ bool fast_ok(const ModelDesc<NSRC> &m, int n) {
-  bool ok = true;
-  const double hi = (double)(n - 1);
-#pragma unroll
-  for (int g = 0; g < 2 * NSRC; ++g) {
-    const Gauss &q = m.g[g];
-    const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
-    const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
-    const double B = fabs(q.k.b) * mx * my;
-    ok = ok && (B < kFastCross) && isfinite(q.k.a) && isfinite(q.k.c) && isfinite(q.amp) &&
-         (q.k.a >= 0.0) && (q.k.c >= 0.0);
-  }
-  return ok;
-}
-
 template <int NSRC, int NT, bool WRITE>
 __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const double2 *DW,
                                              double *vtab, double *out, int n_rt,
@@ -464,29 +447,31 @@ __device__ __forceinline__ double sweep_fast(const ModelDesc<NSRC> &m, const dou
 //   G_(i+S) = G_i * R_i,   R_(i+S) = R_i * K,   K = exp(-2 c S^2)
 // starting from G_i0 = A exp(-Q(i0)) and R_i0 = exp(-(Q(i0+S) - Q(i0))): two multiplies
 // per pixel-Gaussian and no LDS traffic besides the pixel itself.  Rounding grows
-// like m^2/2 ulp after m rows (<= 2048 ulp at 64 rows, typically ~300).  Guard: every
-// value of Q over the grid (max at a corner, Q is convex) stays below kFast2Q, so no
-// G underflows and |Q(i+S) - Q(i)| < kFast2Q keeps R finite.
+// like m^2/2 ulp after m rows (<= 2048 ulp at 64 rows, typically ~300).  Guard
+// (fast_level): Q stays below kFast2Q over the grid, so no G underflows and
+// |Q(i+S) - Q(i)| < kFast2Q keeps R finite.
 constexpr double kFast2Q = 690.0;
 
+// Which sweep a FAST kernel may use for this model (wave-uniform): 2 = FAST2, 1 = the
+// row-table FAST sweep, 0 = exact.  Per Gaussian, with mx = max|dx|, my = max|dy| over
+// the grid: B = |b| mx my bounds the cross term and a mx^2 + B + c my^2 bounds Q.
 template <int NSRC>
-__device__ __forceinline__ bool fast2_ok(const ModelDesc<NSRC> &m, int n) {
-  bool ok = true;
+__device__ __forceinline__ int fast_level(const ModelDesc<NSRC> &m, int n) {
   const double hi = (double)(n - 1);
+  bool ok1 = true, ok2 = true;
 #pragma unroll
   for (int g = 0; g < 2 * NSRC; ++g) {
     const Gauss &q = m.g[g];
-    double qmax = 0.0;
-#pragma unroll
-    for (int cx = 0; cx < 2; ++cx)
-#pragma unroll
-      for (int cy = 0; cy < 2; ++cy) {
-        const double xd = (cx ? hi : 0.0) - q.x0, yd = (cy ? hi : 0.0) - q.y0;
-        qmax = fmax(qmax, (q.k.a * (xd * xd) + (q.k.b * xd) * yd) + q.k.c * (yd * yd));
-      }
-    ok = ok && (qmax < kFast2Q) && isfinite(q.amp) && isfinite(q.k.K);
+    const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
+    const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
+    const double B = fabs(q.k.b) * mx * my;
+    const double Qb = (q.k.a * (mx * mx) + B) + q.k.c * (my * my);
+    const bool fin = isfinite(q.k.a) && isfinite(q.k.c) && isfinite(q.amp) &&
+                     (q.k.a >= 0.0) && (q.k.c >= 0.0);
+    ok1 = ok1 && fin && (B < kFastCross);
+    ok2 = ok2 && fin && (Qb < kFast2Q) && isfinite(q.k.K);
   }
-  return ok;
+  return ok2 ? 2 : (ok1 ? 1 : 0);
 }
 
 template <int NSRC, int NT, bool WRITE>
@@ -546,11 +531,9 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
                                         double *vtab, double *out, int n, int lane) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
   if constexpr (FAST) {
-    const int nn = NT ? NT : n;
-    if (fast_ok<NSRC>(m, nn)) {
-      if (fast2_ok<NSRC>(m, nn)) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
-      return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
-    }
+    const int lvl = fast_level<NSRC>(m, NT ? NT : n);
+    if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
+    if (lvl == 1) return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
     return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
   } else {
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
