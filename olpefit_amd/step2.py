@@ -26,18 +26,23 @@ from . import fitsio, pipeline
 from .core import Sampler
 
 
-def parse(argv, nsrc):
-    ap = argparse.ArgumentParser(prog="apf_step2" if nsrc == 2 else "apf_step2_3body")
+def parse(argv, nsrc, variant="2"):
+    prog = {"2": "apf_step2", "2a": "apf_step2a"}[variant] + ("" if nsrc == 2 else "_3body")
+    ap = argparse.ArgumentParser(prog=prog)
     ap.add_argument("image", type=str)
-    if nsrc == 2:
+    if variant == "2a":
+        # apf_step2a.py: one walker, n_steps = 5000 (:39), no MPI, writes step2a.csv
+        ap.set_defaults(walkers=1, iters=5000, burn_in=0, accept_min=0, initial_guess_option="1")
+    if nsrc == 2 and variant == "2":
         ap.add_argument("-i", "--initial_guess_option", type=str,
                         help="-i 1 for the step 1 guess, -i 2a for the step 2a output")
-    ap.add_argument("--walkers", type=int, default=24,
+    ap.add_argument("--walkers", type=int, default=24 if variant == "2" else 1,
                     help="independent walkers (the reference's MPI processes)")
     ap.add_argument("--accept-min", type=int, default=100000,
                     help="stop when a walker has tried every parameter this often")
-    ap.add_argument("--burn-in", type=int, default=6000 if nsrc == 2 else 0)
-    ap.add_argument("--iters", type=int, default=0,
+    ap.add_argument("--burn-in", type=int,
+                    default=6000 if (nsrc == 2 and variant == "2") else 0)
+    ap.add_argument("--iters", type=int, default=0 if variant == "2" else 5000,
                     help="run exactly this many iterations (overrides --accept-min; use a "
                          "multiple of 10 to mirror the reference's write cadence)")
     ap.add_argument("--seed", type=int, default=None,
@@ -107,8 +112,11 @@ def _parallel(shards, fn):
         raise errs[0]
 
 
-def main(argv=None, nsrc=2):
-    args = parse(sys.argv[1:] if argv is None else argv, nsrc)
+def main(argv=None, nsrc=2, variant="2"):
+    """variant "2": apf_step2 (many walkers, {w}_finalarray_mpi.csv); "2a": the single
+    walker warm-up of apf_step2a.py writing step2a.csv / step2a_acceptance_rate
+    (:324-331), which ``apf_step2.py -i 2a`` then starts from (apf_step2.py:248-256)."""
+    args = parse(sys.argv[1:] if argv is None else argv, nsrc, variant)
     say = (lambda *a: None) if args.quiet else print
     image, hdr = fitsio.getdata_header(args.image)              # apf_step2.py:160-161
     directory, frame, outdir = pipeline.image_paths(args.image)  # :164-170
@@ -175,9 +183,11 @@ def main(argv=None, nsrc=2):
         for k in range(sh.W):
             w = sh.w0 + k
             if not args.no_csv:
-                pipeline.write_chain_csv(outdir + f"{w}_finalarray_mpi.csv",
-                                         pipeline.with_seed_row(chain[k]))
-                pipeline.write_acceptance(outdir + f"{w}_acceptance_rate.csv", acc[k], tries[k])
+                chain_name, acc_name = ((f"{w}_finalarray_mpi.csv", f"{w}_acceptance_rate.csv")
+                                        if variant == "2" else
+                                        ("step2a.csv", "step2a_acceptance_rate"))
+                pipeline.write_chain_csv(outdir + chain_name, pipeline.with_seed_row(chain[k]))
+                pipeline.write_acceptance(outdir + acc_name, acc[k], tries[k])
             if args.npy:
                 np.save(outdir + f"{w}_chain.npy", chain[k])
     say("done with loop")

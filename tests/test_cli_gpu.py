@@ -70,3 +70,19 @@ def test_cli_seeds_are_gpu_count_independent(tmp_path):
         s2.Shard.__init__ = orig
     for w in range(5):
         np.testing.assert_array_equal(np.load(out2 + f"{w}_chain.npy"), one[w])
+
+
+def test_step2a_then_step2_from_2a(tmp_path):
+    """apf_step2a writes step2a.csv (one walker, 5000 steps by default; 300 here);
+    apf_step2 -i 2a starts every walker from its last row (apf_step2.py:248-256)."""
+    path = synth.write_case(str(tmp_path), 32, 2)
+    out = step2.main([path, "--iters", "300", "--seed", "5", "-q"], nsrc=2, variant="2a")
+    a = np.genfromtxt(out + "step2a.csv", delimiter=",")
+    assert a.shape == (301, 17) and np.all(np.isnan(a[0]))
+    assert os.path.exists(out + "step2a_acceptance_rate")
+    out2 = step2.main([path, "-i", "2a", "--walkers", "3", "--iters", "20", "--burn-in", "0",
+                       "--seed", "9", "-q", "--no-csv", "--npy"])
+    c0 = np.load(out2 + "0_chain.npy")
+    # the first row differs from step2a's last row in at most one parameter + chi^2
+    diff = np.nonzero(c0[0, :16] != a[-1, :16])[0]
+    assert diff.size <= 1

@@ -125,3 +125,23 @@ def test_step3_reader_and_gelman_rubin(tmp_path, golden):
                              pipeline.with_seed_row(chains[3][:10]))
     with pytest.raises(ValueError):
         step3.load_chains(str(tmp_path), 4)
+
+
+def test_headless_step1_guess(tmp_path):
+    from olpefit_amd import step1
+    path = synth.write_case(str(tmp_path), 64, 2)
+    img, _ = fitsio.getdata_header(path)
+    p = synth.truth_params(64, 2)
+    out = step1.main([str(tmp_path), "--star", str(p[0] + 2.3), str(p[1] - 1.7),
+                      "--companion", str(p[2] + 1.1), str(p[3] + 0.4), "--sky", "3.7", "2.2"])
+    assert out == [str(tmp_path) + "/00001_initialguess"]
+    g = pipeline.read_guess(out[0])
+    # apf_step1.py:145-152: 21x21 argmax around the truncated click, + 0.5 px
+    ys, xs = np.unravel_index(np.argmax(img), img.shape)
+    assert (g[0], g[1]) == (xs + 0.5, ys + 0.5)
+    assert g[4] == 3 and g[5] == 2
+    box = img[int(p[3] + 0.4) - 11:int(p[3] + 0.4) + 10, int(p[2] + 1.1) - 11:int(p[2] + 1.1) + 10]
+    yc, xc = np.unravel_index(np.argmax(box), box.shape)
+    assert g[2] == int(p[2] + 1.1) - 11 + xc + 0.5 and g[3] == int(p[3] + 0.4) - 11 + yc + 0.5
+    text = open(out[0]).read()
+    assert text.endswith("\n") and len(text.split()) == 6
