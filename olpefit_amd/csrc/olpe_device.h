@@ -501,8 +501,10 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
     }
     const int jj = act ? j : 0;
     const double bg = m.bg;
-#pragma unroll 4
-    for (int i = cw.grp; i < n; i += cw.S) {
+    double K[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) K[g] = m.g[g].k.K;
+    auto row = [&](int i, double2 dw) {
       double mod = Gv[0] + Gv[1];
 #pragma unroll
       for (int s = 1; s < NSRC; ++s) mod = mod + (Gv[2 * s] + Gv[2 * s + 1]);
@@ -510,15 +512,39 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         Gv[g] = Gv[g] * R[g];
-        R[g] = R[g] * m.g[g].k.K;
+        R[g] = R[g] * K[g];
       }
       if constexpr (WRITE) {
         if (act) out[i * n + j] = mod;
       } else {
-        const double2 dw = DW[i * n + jj];
         const double t = fma(-mod, dw.y, dw.x);
         acc = act ? fma(t, t, acc) : acc;
       }
+    };
+    constexpr int BLK = 4;
+    const int rows = (n - cw.grp + cw.S - 1) / cw.S;       // rows of this lane
+    if (!WRITE && NT != 0 && rows % BLK == 0) {
+      // explicit software pipeline: the next block's pixels are loaded into their own
+      // registers while this block computes, so one lgkmcnt wait per block is covered
+      const int rstep = cw.S * n;
+      const double2 *p = DW + cw.grp * n + jj;
+      double2 cur[BLK], nxt[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) cur[k] = p[k * rstep];
+      for (int b0 = 0; b0 < rows; b0 += BLK) {
+        const double2 *pn = p + ((b0 + BLK < rows) ? BLK * rstep : 0);
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) nxt[k] = pn[k * rstep];
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) row(cw.grp + (b0 + k) * cw.S, cur[k]);
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+        p = pn;
+      }
+    } else {
+#pragma unroll 4
+      for (int i = cw.grp; i < n; i += cw.S)
+        row(i, WRITE ? make_double2(0.0, 0.0) : DW[i * n + jj]);
     }
   }
   return acc;
@@ -530,6 +556,14 @@ template <int NSRC, int NT, bool WRITE, bool FAST>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
+#ifdef OLPE_DIAG_NO_SWEEP
+  // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
+  // the remaining per-step cost can be timed; results are meaningless
+  if constexpr (!WRITE) {
+    asm volatile("" ::"v"(m.g[0].amp), "v"(m.bg));
+    return img[lane].x * 1e-300;
+  }
+#endif
   if constexpr (FAST) {
     const int lvl = fast_level<NSRC>(m, NT ? NT : n);
     if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Build a diagnostic libolpe variant into /root/repo/diag/<name>/libolpe.so (never the
+# product library).  usage: tools/diag_build.sh <name> <extra hipcc flags...>
+name=$1; shift
+mkdir -p diag/$name
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off \
+  "$@" -o diag/$name/libolpe.so olpefit_amd/csrc/olpe.hip olpefit_amd/csrc/olpe_comm.hip -lrccl
