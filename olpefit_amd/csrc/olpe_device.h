@@ -566,6 +566,9 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
 #endif
   if constexpr (FAST) {
     const int lvl = fast_level<NSRC>(m, NT ? NT : n);
+    // the descriptor lives in LDS: make the sweeps reload the fields they use instead
+    // of keeping the guard's loads live (and spilled) across the row loop
+    asm volatile("" ::: "memory");
     if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
     if (lvl == 1) return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
     return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
