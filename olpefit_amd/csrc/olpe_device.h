@@ -55,10 +55,29 @@ __device__ __forceinline__ double uniform_f64(double v) {
   return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
 }
 
+// one DPP move of a double (both halves); lanes outside row_mask read 0
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
+// Wave-wide sum with DPP (no LDS round trips): quad_perm [1,0,3,2] / [2,3,0,1],
+// row_half_mirror, row_mirror, row_bcast:15 (rows 1,3), row_bcast:31 (rows 2,3);
+// lane 63 ends with the total, broadcast with readlane.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return uniform_f64(v);
+  v += dpp_f64<0xB1, 0xf>(v);
+  v += dpp_f64<0x4E, 0xf>(v);
+  v += dpp_f64<0x141, 0xf>(v);
+  v += dpp_f64<0x140, 0xf>(v);
+  v += dpp_f64<0x142, 0xa>(v);
+  v += dpp_f64<0x143, 0xc>(v);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
 }
 
 // ---------------------------------------------------------------------------------
