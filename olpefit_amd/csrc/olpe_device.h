@@ -569,6 +569,134 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
   return acc;
 }
 
+// FAST3 evaluation (default path): the Gaussians of one shape set (all narrow ones
+// share sigma_x, sigma_y, theta; all wide ones too) share c, so with k the lane's row
+// step (row i = grp + k*S), a reference step kc and
+//   H_k = exp(-c S^2 (k - kc)(k - kc - 1))            one table per set, k-uniform
+//   a_k = A exp(-(Q_0 - c S^2 kc (kc+1))) * rho^k,   rho = exp(-(Q_1 - Q_0 + 2 c S^2 kc))
+// G_k = a_k * H_k exactly (Q_k is quadratic in k).  a_k is geometric (1 multiply per
+// pixel-Gaussian, <= k ulp), H comes from an LDS table read once per row for all
+// Gaussians:  model = fma(sum_narrow a, H_n, (sum_wide a) * H_w) + bg.
+// 11 FP64 ops per pixel for 2 sources (FAST2: 14).  Guard (fast3_ok): c S^2 (kc+1)^2
+// < 600 keeps a_k from overflowing and H from underflowing, and the FAST2 bound on Q
+// (relaxed by c S^2 kc (kc+1)) keeps a_0 from underflowing where G is significant.
+template <int NSRC>
+__device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int rows, int kc) {
+  const double hi = (double)(n - 1);
+  const double S2 = (double)(row_stride(n) * row_stride(n));
+  const double km = (double)(kc > rows - 1 - kc ? kc : rows - 1 - kc) + 1.0;
+  bool ok = true;
+#pragma unroll
+  for (int g = 0; g < 2 * NSRC; ++g) {
+    const Gauss &q = m.g[g];
+    const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
+    const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
+    const double Qb = (q.k.a * (mx * mx) + fabs(q.k.b) * mx * my) + q.k.c * (my * my);
+    const double cs = q.k.c * S2;
+    ok = ok && (cs * km * km < 600.0) && (Qb < 700.0 + cs * kc * (kc + 1.0)) &&
+         isfinite(Qb) && isfinite(q.amp) && (q.k.a >= 0.0) && (q.k.c >= 0.0);
+  }
+  return ok;
+}
+
+template <int NSRC, int NT, bool WRITE>
+__device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
+                                              double *htab, double *out, int n_rt, int lane,
+                                              int rows, int kc) {
+  constexpr int G = 2 * NSRC;
+  const int n = NT ? NT : n_rt;
+  const ColWalk cw(n, lane);
+  const double S = (double)cw.S;
+  const double cw2 = m.g[0].k.c * (S * S);        // wide set   (even g)
+  const double cn2 = m.g[1].k.c * (S * S);        // narrow set (odd g)
+  // H table: htab[2k] = H_wide(k), htab[2k+1] = H_narrow(k), k lane-parallel
+  for (int k = lane; k < rows; k += 64) {
+    const double dk = (double)(k - kc);
+    const double e = dk * (dk - 1.0);
+    htab[2 * k] = exp(-(cw2 * e));
+    htab[2 * k + 1] = exp(-(cn2 * e));
+  }
+  wave_sync();
+  const double kcd = (double)kc;
+  const double yr = (double)cw.grp;
+  const double bg = m.bg;
+  double acc = 0.0;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int j = c0 + cw.jl;
+    const bool act = cw.lane_ok && j < n;
+    const double xj = (double)j;
+    double av[G], rho[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double xd = xj - m.g[g].x0;
+      const double yd = yr - m.g[g].y0;
+      const double c = m.g[g].k.c;
+      const double cs = c * (S * S);
+      const double bx = m.g[g].k.b * xd;
+      const double q0 = (m.g[g].k.a * (xd * xd) + bx * yd) + c * (yd * yd);
+      const double d0 = bx * S + (c * S) * (2.0 * yd + S);
+      av[g] = m.g[g].amp * exp(-(q0 - cs * (kcd * (kcd + 1.0))));
+      rho[g] = exp(-(d0 + 2.0 * cs * kcd));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int jj = act ? j : 0;
+    const double2 *hr = reinterpret_cast<const double2 *>(htab);
+    auto row = [&](int i, double2 h, double2 dw) {
+      double sw = av[0], sn = av[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) {
+        sw = sw + av[2 * s];
+        sn = sn + av[2 * s + 1];
+      }
+      const double mod = fma(sn, h.y, sw * h.x) + bg;
+#pragma unroll
+      for (int g = 0; g < G; ++g) av[g] = av[g] * rho[g];
+      if constexpr (WRITE) {
+        if (act) out[i * n + j] = mod;
+      } else {
+        const double t = fma(-mod, dw.y, dw.x);
+        acc = act ? fma(t, t, acc) : acc;
+      }
+    };
+    constexpr int BLK = 4;
+    if (!WRITE && NT != 0 && rows % BLK == 0) {
+      const int rstep = cw.S * n;
+      const double2 *p = DW + cw.grp * n + jj;
+      double2 cur[BLK], nxt[BLK], hc[BLK], hn[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) {
+        cur[k] = p[k * rstep];
+        hc[k] = hr[k];
+      }
+      for (int b0 = 0; b0 < rows; b0 += BLK) {
+        const bool more = b0 + BLK < rows;
+        const double2 *pn = p + (more ? BLK * rstep : 0);
+        const int hb = more ? b0 + BLK : b0;
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) {
+          nxt[k] = pn[k * rstep];
+          hn[k] = hr[hb + k];
+        }
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) row(cw.grp + (b0 + k) * cw.S, hc[k], cur[k]);
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) {
+          cur[k] = nxt[k];
+          hc[k] = hn[k];
+        }
+        p = pn;
+      }
+    } else {
+      int k = 0;
+#pragma unroll 2
+      for (int i = cw.grp; i < n; i += cw.S, ++k)
+        row(i, hr[k], WRITE ? make_double2(0.0, 0.0) : DW[i * n + jj]);
+    }
+  }
+  wave_sync();   // htab is rewritten by the next step
+  return acc;
+}
+
 // FAST kernels keep the exact sweep only as the (rare) fallback, unrolled once so
 // that it does not set the kernel's register budget.
 template <int NSRC, int NT, bool WRITE, bool FAST>
@@ -584,7 +712,14 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
   }
 #endif
   if constexpr (FAST) {
-    const int lvl = fast_level<NSRC>(m, NT ? NT : n);
+    const int nn = NT ? NT : n;
+    const ColWalk cw(nn, lane);
+    const int rows = (nn - cw.grp + cw.S - 1) / cw.S;    // uniform when S divides n
+    const int kc = rows / 2;
+    const bool ok3 = fast3_ok<NSRC>(m, nn, rows, kc);
+    asm volatile("" ::: "memory");
+    if (ok3) return sweep_fast3<NSRC, NT, WRITE>(m, img, vtab, out, n, lane, rows, kc);
+    const int lvl = fast_level<NSRC>(m, nn);
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
     // of keeping the guard's loads live (and spilled) across the row loop
     asm volatile("" ::: "memory");
