@@ -55,13 +55,14 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
     exact: per pixel-Gaussian 7 ops + one exp, per pixel G-1 combines + background +
            3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel G
-           multiplies + G-1 adds + background + 2 fma (residual, accumulate); per
+           multiplies + G-2 adds + 2 fma (the two shape tables, background folded in)
+           + 2 fma (residual, accumulate); per
            Gaussian and column 2 exps + 10 ops (the geometric row factor a_k and the
            column term); per row 2 exps + 6 ops (the shared shape table H)."""
     g = 2 * nsrc
     if mode == "exact":
         return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
-    return n * n * (2 * g + 3) + n * g * (2 * EXP_OPS + 10) + 2 * n * (EXP_OPS + 3)
+    return n * n * (2 * g + 2) + n * g * (2 * EXP_OPS + 10) + 2 * n * (EXP_OPS + 3)
 
 
 def sec8d_work(n: int, nsrc: int) -> float:

@@ -165,6 +165,16 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     ndone = __builtin_amdgcn_readfirstlane(ndone);
   }
 
+  // chain rows: the next count that records (count >= burn_in, (count - burn_in) %
+  // stride == 0) and its row, advanced by addition (no 64-bit division per step)
+  long long rec_next = -1, rec_row = 0;
+  if (A.stride > 0) {
+    const long long c1 = A.count0 + 1;
+    const long long k = c1 > A.burn_in ? (c1 - A.burn_in + A.stride - 1) / A.stride : 0;
+    rec_next = A.burn_in + k * A.stride;
+    rec_row = k - A.row0;
+  }
+
   long long count = A.count0;
   for (long long it = 0; it < A.n_iters; ++it) {
     // randint(0, NP)  (apf_step2.py:302)
@@ -249,10 +259,11 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       t[5] = acc ? 1.0 : 0.0;
     }
     // chain record (:342-351, generalised to a stride)
-    if (A.stride > 0 && count >= A.burn_in && (count - A.burn_in) % A.stride == 0) {
-      const long long row = (count - A.burn_in) / A.stride - A.row0;
-      if (row >= 0 && row < A.nrows && lane < PS)
-        A.chain[((size_t)w * A.nrows + row) * PS + lane] = st[lane];
+    if (count == rec_next) {
+      if (rec_row >= 0 && rec_row < A.nrows && lane < PS)
+        A.chain[((size_t)w * A.nrows + rec_row) * PS + lane] = st[lane];
+      rec_next += A.stride;
+      ++rec_row;
     }
   }
 

@@ -576,27 +576,26 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
 //   a_k = A exp(-(Q_0 - c S^2 kc (kc+1))) * rho^k,   rho = exp(-(Q_1 - Q_0 + 2 c S^2 kc))
 // G_k = a_k * H_k exactly (Q_k is quadratic in k).  a_k is geometric (1 multiply per
 // pixel-Gaussian, <= k ulp), H comes from an LDS table read once per row for all
-// Gaussians:  model = fma(sum_narrow a, H_n, (sum_wide a) * H_w) + bg.
-// 11 FP64 ops per pixel for 2 sources (FAST2: 14).  Guard (fast3_ok): c S^2 (kc+1)^2
+// Gaussians:  model = fma(sum_narrow a, H_n, fma(sum_wide a, H_w, bg)).
+// 10 FP64 ops per pixel for 2 sources (FAST2: 14).  Guard (fast3_ok): c S^2 (kc+1)^2
 // < 600 keeps a_k from overflowing and H from underflowing, and the FAST2 bound on Q
 // (relaxed by c S^2 kc (kc+1)) keeps a_0 from underflowing where G is significant.
+// Lane-parallel: lane g < 2*NSRC tests Gaussian g (the descriptor is in LDS), one
+// ballot combines them.
 template <int NSRC>
-__device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int rows, int kc) {
+__device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int rows, int kc,
+                                         int lane) {
   const double hi = (double)(n - 1);
   const double S2 = (double)(row_stride(n) * row_stride(n));
   const double km = (double)(kc > rows - 1 - kc ? kc : rows - 1 - kc) + 1.0;
-  bool ok = true;
-#pragma unroll
-  for (int g = 0; g < 2 * NSRC; ++g) {
-    const Gauss &q = m.g[g];
-    const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
-    const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
-    const double Qb = (q.k.a * (mx * mx) + fabs(q.k.b) * mx * my) + q.k.c * (my * my);
-    const double cs = q.k.c * S2;
-    ok = ok && (cs * km * km < 600.0) && (Qb < 700.0 + cs * kc * (kc + 1.0)) &&
-         isfinite(Qb) && isfinite(q.amp) && (q.k.a >= 0.0) && (q.k.c >= 0.0);
-  }
-  return ok;
+  const Gauss &q = m.g[lane < 2 * NSRC ? lane : 0];
+  const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
+  const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
+  const double Qb = (q.k.a * (mx * mx) + fabs(q.k.b) * mx * my) + q.k.c * (my * my);
+  const double cs = q.k.c * S2;
+  const bool ok = (cs * km * km < 600.0) && (Qb < 700.0 + cs * kc * (kc + 1.0)) &&
+                  isfinite(Qb) && isfinite(q.amp) && (q.k.a >= 0.0) && (q.k.c >= 0.0);
+  return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
 template <int NSRC, int NT, bool WRITE>
@@ -648,7 +647,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         sw = sw + av[2 * s];
         sn = sn + av[2 * s + 1];
       }
-      const double mod = fma(sn, h.y, sw * h.x) + bg;
+      const double mod = fma(sn, h.y, fma(sw, h.x, bg));
 #pragma unroll
       for (int g = 0; g < G; ++g) av[g] = av[g] * rho[g];
       if constexpr (WRITE) {
@@ -716,7 +715,7 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     const ColWalk cw(nn, lane);
     const int rows = (nn - cw.grp + cw.S - 1) / cw.S;    // uniform when S divides n
     const int kc = rows / 2;
-    const bool ok3 = fast3_ok<NSRC>(m, nn, rows, kc);
+    const bool ok3 = fast3_ok<NSRC>(m, nn, rows, kc, lane);
     asm volatile("" ::: "memory");
     if (ok3) return sweep_fast3<NSRC, NT, WRITE>(m, img, vtab, out, n, lane, rows, kc);
     const int lvl = fast_level<NSRC>(m, nn);
