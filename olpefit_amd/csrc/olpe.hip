@@ -68,6 +68,21 @@ struct GibbsArgs {
 
 constexpr int kTraceF = 6;
 
+// Diagnostic build only (tools/diag_build.sh ... -DOLPE_DIAG_TIMING): per-wave cycle
+// totals of the step's sections (s_memtime), written over the trace buffer at the end.
+#ifdef OLPE_DIAG_TIMING
+#define DT_MARK(i)                                             \
+  do {                                                         \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    dt[i] += _t - dt_last;                                     \
+    dt_last = _t;                                              \
+  } while (0)
+#else
+#define DT_MARK(i) \
+  do {             \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------
 // The fused sampler
 // ---------------------------------------------------------------------------------
@@ -77,10 +92,10 @@ template <int NP> struct WaveSlice {
   static constexpr int U32 = MT_N + 2 * NP;                  // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
   static constexpr int NSRC = NP == 16 ? 2 : 3;
-  // doubles: params[PS] | T1[3] T2[3] | C1[4] C2[4] | pending T[3] C[4]
-  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 10;
-  static constexpr int OPT = PS + 14, OPC = PS + 17;
-  static constexpr int F64 = PS + 21;
+  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
+  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
+  static constexpr int OPT = PS + 12, OPC = PS + 15;
+  static constexpr int F64 = PS + 18;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
   static constexpr int BYTES = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
 };
@@ -89,12 +104,12 @@ __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsr
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
-__device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2], s[3]}; }
+__device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }
 __device__ __forceinline__ void st_trig(double *s, const Trig &t) {
   s[0] = t.cost2; s[1] = t.sint2; s[2] = t.sin2t;
 }
 __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
-  s[0] = k.a; s[1] = k.b; s[2] = k.c; s[3] = k.K;
+  s[0] = k.a; s[1] = k.b; s[2] = k.c;
 }
 
 template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
@@ -105,7 +120,6 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = NT ? NT : A.n;
   const int npix = n * n;
-  const double RS = (double)row_stride(n);
   const int lane = threadIdx.x & 63;
   // wave index as a provably uniform (SGPR) value: LDS slice addresses stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,11 +155,11 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   if (lane < PS) st[lane] = A.state[w * PS + lane];
   wave_sync();
   if (lane == 0) {
-    const Trig t1 = make_trig(st[L::T1]), t2 = make_trig(st[L::T2]);
+    const Trig t1 = make_trig<FAST>(st[L::T1]), t2 = make_trig<FAST>(st[L::T2]);
     st_trig(st + WS::OT1, t1);
     st_trig(st + WS::OT2, t2);
-    st_coef(st + WS::OC1, make_coef(st[L::S1X], st[L::S1Y], t1, RS));
-    st_coef(st + WS::OC2, make_coef(st[L::S2X], st[L::S2Y], t2, RS));
+    st_coef(st + WS::OC1, make_coef<FAST>(st[L::S1X], st[L::S1Y], t1));
+    st_coef(st + WS::OC2, make_coef<FAST>(st[L::S2X], st[L::S2Y], t2));
   }
   wave_sync();
 
@@ -175,7 +189,13 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     rec_row = k - A.row0;
   }
 
+  HCache hcache;
+  __builtin_amdgcn_s_setprio(1);
   long long count = A.count0;
+#ifdef OLPE_DIAG_TIMING
+  unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long dt_last = __builtin_amdgcn_s_memtime();
+#endif
   for (long long it = 0; it < A.n_iters; ++it) {
     // randint(0, NP)  (apf_step2.py:302)
     const int r = __builtin_amdgcn_readfirstlane(mt.template randint<NP>(lane));
@@ -184,6 +204,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     wave_sync();
     if (lane == 0) s_tries[r] = tr;
     if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) ++ndone;
+    DT_MARK(0);
 
     // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
     const double cur = uniform_f64(st[r]);
@@ -197,6 +218,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       nv = cur + wr * g;
     }
     nv = uniform_f64(nv);
+    DT_MARK(1);
 
     // coefficient sets of the proposal: only the set that r touches is rebuilt
     auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
@@ -204,15 +226,15 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
                   : (r == L::S2X || r == L::S2Y || r == L::T2) ? 2 : 0;
     Coef C1p, C2p;
     if (grp == 1) {
-      const Trig t = (r == L::T1) ? make_trig(nv) : ld_trig(st + WS::OT1);
-      C1p = make_coef(q(L::S1X), q(L::S1Y), t, RS);
+      const Trig t = (r == L::T1) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT1);
+      C1p = make_coef<FAST>(q(L::S1X), q(L::S1Y), t);
       if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
     } else {
       C1p = ld_coef(st + WS::OC1);
     }
     if (grp == 2) {
-      const Trig t = (r == L::T2) ? make_trig(nv) : ld_trig(st + WS::OT2);
-      C2p = make_coef(q(L::S2X), q(L::S2Y), t, RS);
+      const Trig t = (r == L::T2) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT2);
+      C2p = make_coef<FAST>(q(L::S2X), q(L::S2Y), t);
       if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
     } else {
       C2p = ld_coef(st + WS::OC2);
@@ -224,15 +246,24 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       if (lane == 0) *mdl = md;
     }
     wave_sync();
+    DT_MARK(2);
 
     // build_analytical_model + chi_squared (:314-316)
-    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane);
+    // the step's scalar control is a latency-bound chain: it runs at raised wave
+    // priority so that it is not queued behind the other waves' sweeps
+    __builtin_amdgcn_s_setprio(0);
+    hcache.grp = grp;
+    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, &hcache);
+    __builtin_amdgcn_s_setprio(1);
+    DT_MARK(3);
     const double chi = wave_sum(part);
+    DT_MARK(4);
 
     // accept_reject (:139-148)
     const double p_accept = exp(-(chi - st[PS - 1]) / 2.);
     const double dice = mt.rand53(lane);
     const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
+    hcache.after(acc);
     wave_sync();
     if (acc && lane == 0) {
       s_acc[r] = s_acc[r] + 1u;
@@ -242,13 +273,15 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
         double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
         double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
         for (int k = 0; k < 3; ++k) dt[k] = st[WS::OPT + k];
-        for (int k = 0; k < 4; ++k) dc[k] = st[WS::OPC + k];
+        for (int k = 0; k < 3; ++k) dc[k] = st[WS::OPC + k];
       }
     }
     wave_sync();
     ++count;
     if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = count;
+    DT_MARK(5);
 
+#ifndef OLPE_DIAG_TIMING
     if (A.trace && lane == 0) {
       double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
       t[0] = (double)r;
@@ -258,6 +291,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       t[4] = p_accept;
       t[5] = acc ? 1.0 : 0.0;
     }
+#endif
     // chain record (:342-351, generalised to a stride)
     if (count == rec_next) {
       if (rec_row >= 0 && rec_row < A.nrows && lane < PS)
@@ -265,7 +299,15 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       rec_next += A.stride;
       ++rec_row;
     }
+    DT_MARK(6);
   }
+#ifdef OLPE_DIAG_TIMING
+  if (A.trace && lane < 7) {
+    unsigned long long v = 0;
+    for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
+    A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
+  }
+#endif
 
   // ---- write back
   wave_sync();
@@ -301,15 +343,22 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n
   double p[PS];
 #pragma unroll
   for (int k = 0; k < PS; ++k) p[k] = uniform_f64(params[w * PS + k]);
-  const Trig T1 = make_trig(p[L::T1]), T2 = make_trig(p[L::T2]);
-  const double RS = (double)row_stride(n);
-  const Coef C1 = make_coef(p[L::S1X], p[L::S1Y], T1, RS);
-  const Coef C2 = make_coef(p[L::S2X], p[L::S2Y], T2, RS);
   auto q = [&](int k) -> double { return p[k]; };
-  const ModelDesc<NSRC> md = make_model<NSRC>(q, C1, C2, bkgd_mode);
   double *o = WRITE ? out + (size_t)w * n * n : nullptr;
-  const double part = fast ? sweep<NSRC, 0, WRITE, true>(md, DE, vtab, o, n, lane)
-                           : sweep<NSRC, 0, WRITE, false>(md, DE, vtab, o, n, lane);
+  double part;
+  if (fast) {
+    const Trig T1 = make_trig<true>(p[L::T1]), T2 = make_trig<true>(p[L::T2]);
+    const ModelDesc<NSRC> md = make_model<NSRC>(
+        q, make_coef<true>(p[L::S1X], p[L::S1Y], T1), make_coef<true>(p[L::S2X], p[L::S2Y], T2),
+        bkgd_mode);
+    part = sweep<NSRC, 0, WRITE, true>(md, DE, vtab, o, n, lane);
+  } else {
+    const Trig T1 = make_trig<false>(p[L::T1]), T2 = make_trig<false>(p[L::T2]);
+    const ModelDesc<NSRC> md = make_model<NSRC>(
+        q, make_coef<false>(p[L::S1X], p[L::S1Y], T1),
+        make_coef<false>(p[L::S2X], p[L::S2Y], T2), bkgd_mode);
+    part = sweep<NSRC, 0, WRITE, false>(md, DE, vtab, o, n, lane);
+  }
   if constexpr (!WRITE) {
     const double chi = wave_sum(part);
     if (lane == 0) out[w] = chi;

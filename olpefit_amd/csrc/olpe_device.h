@@ -208,27 +208,36 @@ struct Trig {
 };
 struct Coef {
   double a, b, c;
-  double K;   // exp(-2 c S^2): row-step factor of sweep_fast2's second-order recurrence
 };
 struct Gauss {
   double amp, x0, y0;
   Coef k;
 };
 
+// EXACT keeps astropy's operations (np.sin(2*theta), six divisions); FAST kernels use
+// sin(2t) = 2 sin(t) cos(t) and two reciprocals (<= 2 ulp apart, within the fast
+// tolerances of DESIGN.md §5).
+template <bool FAST>
 __device__ __forceinline__ Trig make_trig(double th) {
   double s, c;
   sincos(th, &s, &c);          // np.sin(theta), np.cos(theta): one range reduction
-  return Trig{c * c, s * s, sin(2. * th)};
+  return Trig{c * c, s * s, FAST ? 2.0 * (s * c) : sin(2. * th)};
 }
 
-__device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t,
-                                          double S = 1.0) {
+template <bool FAST>
+__device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t) {
   const double xstd2 = sx * sx, ystd2 = sy * sy;
   Coef k;
-  k.a = 0.5 * ((t.cost2 / xstd2) + (t.sint2 / ystd2));
-  k.b = 0.5 * ((t.sin2t / xstd2) - (t.sin2t / ystd2));
-  k.c = 0.5 * ((t.sint2 / xstd2) + (t.cost2 / ystd2));
-  k.K = exp(-(2.0 * k.c * (S * S)));
+  if constexpr (FAST) {
+    const double ix = 1.0 / xstd2, iy = 1.0 / ystd2;
+    k.a = 0.5 * (t.cost2 * ix + t.sint2 * iy);
+    k.b = 0.5 * (t.sin2t * (ix - iy));
+    k.c = 0.5 * (t.sint2 * ix + t.cost2 * iy);
+  } else {
+    k.a = 0.5 * ((t.cost2 / xstd2) + (t.sint2 / ystd2));
+    k.b = 0.5 * ((t.sin2t / xstd2) - (t.sin2t / ystd2));
+    k.c = 0.5 * ((t.sint2 / xstd2) + (t.cost2 / ystd2));
+  }
   return k;
 }
 
@@ -488,7 +497,7 @@ __device__ __forceinline__ int fast_level(const ModelDesc<NSRC> &m, int n) {
     const bool fin = isfinite(q.k.a) && isfinite(q.k.c) && isfinite(q.amp) &&
                      (q.k.a >= 0.0) && (q.k.c >= 0.0);
     ok1 = ok1 && fin && (B < kFastCross);
-    ok2 = ok2 && fin && (Qb < kFast2Q) && isfinite(q.k.K);
+    ok2 = ok2 && fin && (Qb < kFast2Q);
   }
   return ok2 ? 2 : (ok1 ? 1 : 0);
 }
@@ -520,9 +529,9 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
     }
     const int jj = act ? j : 0;
     const double bg = m.bg;
-    double K[G];
+    double K[G];      // exp(-2 c S^2): the row step of the second-order recurrence
 #pragma unroll
-    for (int g = 0; g < G; ++g) K[g] = m.g[g].k.K;
+    for (int g = 0; g < G; ++g) K[g] = exp(-(2.0 * m.g[g].k.c * (S * S)));
     auto row = [&](int i, double2 dw) {
       double mod = Gv[0] + Gv[1];
 #pragma unroll
@@ -598,24 +607,51 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
+// FAST3's shape tables, tab[2k] = H_wide(k), tab[2k+1] = H_narrow(k), k lane-parallel.
+// `which` selects the sets recomputed (bit 0 wide, bit 1 narrow); the others are copied
+// from `from` (the table of the current state: a Gibbs step changes at most one set).
+template <int NSRC>
+__device__ __forceinline__ void build_htab(const ModelDesc<NSRC> &m, double *tab,
+                                           const double *from, int which, int rows, int kc,
+                                           double S, int lane) {
+  const double cw2 = m.g[0].k.c * (S * S);        // wide set   (even g)
+  const double cn2 = m.g[1].k.c * (S * S);        // narrow set (odd g)
+  for (int k = lane; k < rows; k += 64) {
+    const double dk = (double)(k - kc);
+    const double e = dk * (dk - 1.0);
+    double2 h;
+    h.x = (which & 1) ? exp(-(cw2 * e)) : from[2 * k];
+    h.y = (which & 2) ? exp(-(cn2 * e)) : from[2 * k + 1];
+    reinterpret_cast<double2 *>(tab)[k] = h;
+  }
+  wave_sync();
+}
+
+// Per-walker cache of the FAST3 tables in the two halves of the wave's vtab area: slot
+// `cur` holds the tables of the current state when `valid`; a shape proposal builds its
+// tables in the other slot (`flip` = that slot holds the proposal's tables).
+struct HCache {
+  int cur = 0;
+  bool valid = false;
+  int grp = 0;          // this step's proposal: 0 no shape change, 1 narrow set, 2 wide set
+  bool flip = false;
+  __device__ __forceinline__ void after(bool accepted) {
+    if (accepted && grp) {
+      if (flip) cur ^= 1;
+      else valid = false;
+    }
+    flip = false;
+  }
+};
+
 template <int NSRC, int NT, bool WRITE>
 __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
-                                              double *htab, double *out, int n_rt, int lane,
-                                              int rows, int kc) {
+                                              const double *htab, double *out, int n_rt,
+                                              int lane, int rows, int kc) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
   const ColWalk cw(n, lane);
   const double S = (double)cw.S;
-  const double cw2 = m.g[0].k.c * (S * S);        // wide set   (even g)
-  const double cn2 = m.g[1].k.c * (S * S);        // narrow set (odd g)
-  // H table: htab[2k] = H_wide(k), htab[2k+1] = H_narrow(k), k lane-parallel
-  for (int k = lane; k < rows; k += 64) {
-    const double dk = (double)(k - kc);
-    const double e = dk * (dk - 1.0);
-    htab[2 * k] = exp(-(cw2 * e));
-    htab[2 * k + 1] = exp(-(cn2 * e));
-  }
-  wave_sync();
   const double kcd = (double)kc;
   const double yr = (double)cw.grp;
   const double bg = m.bg;
@@ -692,7 +728,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         row(i, hr[k], WRITE ? make_double2(0.0, 0.0) : DW[i * n + jj]);
     }
   }
-  wave_sync();   // htab is rewritten by the next step
+  wave_sync();   // the tables may be rewritten by the next step
   return acc;
 }
 
@@ -700,7 +736,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // that it does not set the kernel's register budget.
 template <int NSRC, int NT, bool WRITE, bool FAST>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
-                                        double *vtab, double *out, int n, int lane) {
+                                        double *vtab, double *out, int n, int lane,
+                                        HCache *hc = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
@@ -714,16 +751,41 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     const int nn = NT ? NT : n;
     const ColWalk cw(nn, lane);
     const int rows = (nn - cw.grp + cw.S - 1) / cw.S;    // uniform when S divides n
-    const int kc = rows / 2;
-    const bool ok3 = fast3_ok<NSRC>(m, nn, rows, kc, lane);
+    const int rows0 = (nn + cw.S - 1) / cw.S;             // rows of row group 0 (most)
+    const int kc = rows0 / 2;
+    const bool ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
     asm volatile("" ::: "memory");
-    if (ok3) return sweep_fast3<NSRC, NT, WRITE>(m, img, vtab, out, n, lane, rows, kc);
+    if (ok3) {
+      const int tw = 2 * rows0;                            // doubles per slot
+      const double *h;
+      if (!hc) {
+        build_htab<NSRC>(m, vtab, vtab, 3, rows0, kc, (double)cw.S, lane);
+        h = vtab;
+      } else if (hc->grp == 0) {
+        if (!hc->valid) {
+          build_htab<NSRC>(m, vtab + hc->cur * tw, vtab, 3, rows0, kc, (double)cw.S, lane);
+          hc->valid = true;
+        }
+        h = vtab + hc->cur * tw;
+      } else {
+        double *dst = vtab + (hc->cur ^ 1) * tw;
+        build_htab<NSRC>(m, dst, vtab + hc->cur * tw, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3,
+                         rows0, kc, (double)cw.S, lane);
+        hc->flip = true;
+        h = dst;
+      }
+      asm volatile("" ::: "memory");
+      return sweep_fast3<NSRC, NT, WRITE>(m, img, h, out, n, lane, rows, kc);
+    }
     const int lvl = fast_level<NSRC>(m, nn);
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
     // of keeping the guard's loads live (and spilled) across the row loop
     asm volatile("" ::: "memory");
     if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
-    if (lvl == 1) return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+    if (lvl == 1) {
+      if (hc) hc->valid = false;                           // the V table overwrites vtab
+      return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+    }
     return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
   } else {
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);

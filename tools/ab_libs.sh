@@ -1,0 +1,9 @@
+#!/bin/bash
+# A/B the product library against diagnostic variants: tools/ab_libs.sh name1 name2 ...
+B="python bench.py --no-cpu-baseline --no-alt --steps 8"
+for rep in 1 2; do
+  echo "base $($B | python -c 'import json,sys; d=json.loads(sys.stdin.readline()); print(round(d["value"]/1e6,1), "M  kernel_ms", round(d["roofline"]["kernel_ms"],2))')"
+  for v in "$@"; do
+    echo "$v $(OLPE_LIB=diag/$v/libolpe.so $B | python -c 'import json,sys; d=json.loads(sys.stdin.readline()); print(round(d["value"]/1e6,1), "M  kernel_ms", round(d["roofline"]["kernel_ms"],2))')"
+  done
+done
