@@ -47,22 +47,24 @@ CONFIG_NAMES = {
 }
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
 EXP_OPS = 20                      # FP64 VALU ops of one ocml exp(f64)
+EXP_TAB_OPS = 12                  # FP64 VALU ops of olpe::exp_tab (FAST3 setup)
 
 
 def work_per_step(n: int, nsrc: int, mode: str) -> float:
     """FP64 VALU lane-ops of one walker-step's model + chi^2 evaluation.
 
-    exact: per pixel-Gaussian 7 ops + one exp, per pixel G-1 combines + background +
-           3 residual ops, per column-Gaussian 4 hoisted ops.
+    exact: per pixel-Gaussian 7 ops + one exp (E = 20), per pixel G-1 combines +
+           background + 3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel G
            multiplies + G-2 adds + 2 fma (the two shape tables, background folded in)
-           + 2 fma (residual, accumulate); per
-           Gaussian and column 2 exps + 10 ops (the geometric row factor a_k and the
-           column term); per row 2 exps + 6 ops (the shared shape table H)."""
+           + 2 fma (residual, accumulate); per Gaussian and column 2 table exps
+           (E_TAB = 12) + 10 ops; the shape tables are cached across steps and rebuilt
+           for one set (one exp + 3 ops per row) on the 6 of 16 parameter draws that
+           change a shape."""
     g = 2 * nsrc
     if mode == "exact":
         return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
-    return n * n * (2 * g + 2) + n * g * (2 * EXP_OPS + 10) + 2 * n * (EXP_OPS + 3)
+    return n * n * (2 * g + 2) + n * g * (2 * EXP_TAB_OPS + 10) + n * (EXP_TAB_OPS + 3) * 6 / 16
 
 
 def sec8d_work(n: int, nsrc: int) -> float:

@@ -124,8 +124,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   // wave index as a provably uniform (SGPR) value: LDS slice addresses stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 
-  // ---- LDS carve: [DE] (if staged) then one {WaveSlice, V table} per wave
-  double2 *sDE = reinterpret_cast<double2 *>(smem);
+  // ---- LDS carve: exp table, [DE] (if staged), then one {WaveSlice, V table} per wave
+  double *etab = reinterpret_cast<double *>(smem);
+  double2 *sDE = reinterpret_cast<double2 *>(smem + kEtabBytes);
   const int wstride = WS::BYTES + vtab_bytes(n, NSRC);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (size_t)wave * wstride;
@@ -139,8 +140,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   if constexpr (LDS_IMG) {
     // one coalesced 16-B-per-lane staging pass of {data, 1/err}
     for (int k = threadIdx.x; k < npix; k += blockDim.x) sDE[k] = A.DE[k];
-    __syncthreads();
   }
+  if (threadIdx.x < 64) etab[threadIdx.x] = c_exp2_64[threadIdx.x];
+  __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
 
   const long long w = (long long)blockIdx.x * WPB + wave;
@@ -253,7 +255,8 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     // priority so that it is not queued behind the other waves' sweeps
     __builtin_amdgcn_s_setprio(0);
     hcache.grp = grp;
-    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, &hcache);
+    const double part =
+        sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab, &hcache);
     __builtin_amdgcn_s_setprio(1);
     DT_MARK(3);
     const double chi = wave_sum(part);
@@ -337,7 +340,11 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double *vtab = reinterpret_cast<double *>(smem + (size_t)wave * vtab_bytes(n, NSRC));
+  double *etab = reinterpret_cast<double *>(smem);
+  double *vtab =
+      reinterpret_cast<double *>(smem + kEtabBytes + (size_t)wave * vtab_bytes(n, NSRC));
+  if (threadIdx.x < 64) etab[threadIdx.x] = c_exp2_64[threadIdx.x];
+  __syncthreads();
   const long long w = (long long)blockIdx.x * (blockDim.x / 64) + wave;
   if (w >= W) return;
   double p[PS];
@@ -351,13 +358,13 @@ __global__ __launch_bounds__(256) void olpe_eval_kernel(const double2 *DE, int n
     const ModelDesc<NSRC> md = make_model<NSRC>(
         q, make_coef<true>(p[L::S1X], p[L::S1Y], T1), make_coef<true>(p[L::S2X], p[L::S2Y], T2),
         bkgd_mode);
-    part = sweep<NSRC, 0, WRITE, true>(md, DE, vtab, o, n, lane);
+    part = sweep<NSRC, 0, WRITE, true>(md, DE, vtab, o, n, lane, etab);
   } else {
     const Trig T1 = make_trig<false>(p[L::T1]), T2 = make_trig<false>(p[L::T2]);
     const ModelDesc<NSRC> md = make_model<NSRC>(
         q, make_coef<false>(p[L::S1X], p[L::S1Y], T1),
         make_coef<false>(p[L::S2X], p[L::S2Y], T2), bkgd_mode);
-    part = sweep<NSRC, 0, WRITE, false>(md, DE, vtab, o, n, lane);
+    part = sweep<NSRC, 0, WRITE, false>(md, DE, vtab, o, n, lane, etab);
   }
   if constexpr (!WRITE) {
     const double chi = wave_sum(part);
@@ -464,7 +471,7 @@ size_t wave_lds(int n, int np) {
 }
 
 size_t lds_bytes(const olpe_ctx *c, int wpb) {
-  size_t b = (size_t)wpb * wave_lds(c->n, c->np);
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np) + kEtabBytes;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   return b;
 }
@@ -577,7 +584,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->ps = c->np + 1;
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
-  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) <= 160 * 1024;
+  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) + kEtabBytes <= 160 * 1024;
   if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
   std::vector<double2> hDE(npix), hDW(npix);
@@ -656,7 +663,7 @@ static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, boo
   HIPCHK(hipMemcpyAsync(c->d_scratch, params, pin * 8, hipMemcpyHostToDevice, c->stream));
   const int wpb = 4;
   dim3 grid((W + wpb - 1) / wpb), block(wpb * 64);
-  const size_t shm = (size_t)wpb * vtab_bytes(c->n, c->nsrc);
+  const size_t shm = (size_t)wpb * vtab_bytes(c->n, c->nsrc) + kEtabBytes;
   const int fast = c->eval_mode == OLPE_EVAL_FAST;
   if (shm > 65536) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
   if (c->nsrc == 2) {

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "exp_table.h"
+
 namespace olpe {
 
 // ---------------------------------------------------------------------------------
@@ -203,6 +205,29 @@ __device__ inline void mt_seed_serial(uint32_t *key, uint32_t s) {
 // ---------------------------------------------------------------------------------
 // Model pieces (astropy 4.3.1 Gaussian2D.evaluate, functional_models.py:366-381)
 // ---------------------------------------------------------------------------------
+// exp(x) for the FAST3 setup (guarded arguments): x = (64 k + j) ln2/64 + r with
+// |r| <= ln2/128, exp(x) = 2^k * T[j] * (1 + q(r)), q of degree 5, T = 2^(j/64) from an
+// LDS copy of c_exp2_64.  12 FP64 operations instead of ocml's 19 plus range selects;
+// <= 1.13 ulp (tools/gen_exp_table.py --check).  Arguments are clamped to [-745, 709].
+constexpr int kEtabBytes = 64 * 8;
+struct ExpTab {
+  const double *T;
+  __device__ __forceinline__ double operator()(double x) const {
+    x = fmin(fmax(x, -745.0), 709.0);
+    const double kd = __builtin_rint(x * kExpInv);
+    double r = fma(-kd, kExpHi, x);
+    r = fma(-kd, kExpLo, r);
+    double p = fma(r, 1.0 / 120, 1.0 / 24);
+    p = fma(r, p, 1.0 / 6);
+    p = fma(r, p, 0.5);
+    p = fma(r, p, 1.0);
+    const double q = r * p;
+    const int k = (int)kd;
+    const double t = T[k & 63];
+    return ldexp(fma(t, q, t), k >> 6);
+  }
+};
+
 struct Trig {
   double cost2, sint2, sin2t;
 };
@@ -613,15 +638,15 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
 template <int NSRC>
 __device__ __forceinline__ void build_htab(const ModelDesc<NSRC> &m, double *tab,
                                            const double *from, int which, int rows, int kc,
-                                           double S, int lane) {
+                                           double S, int lane, ExpTab ex) {
   const double cw2 = m.g[0].k.c * (S * S);        // wide set   (even g)
   const double cn2 = m.g[1].k.c * (S * S);        // narrow set (odd g)
   for (int k = lane; k < rows; k += 64) {
     const double dk = (double)(k - kc);
     const double e = dk * (dk - 1.0);
     double2 h;
-    h.x = (which & 1) ? exp(-(cw2 * e)) : from[2 * k];
-    h.y = (which & 2) ? exp(-(cn2 * e)) : from[2 * k + 1];
+    h.x = (which & 1) ? ex(-(cw2 * e)) : from[2 * k];
+    h.y = (which & 2) ? ex(-(cn2 * e)) : from[2 * k + 1];
     reinterpret_cast<double2 *>(tab)[k] = h;
   }
   wave_sync();
@@ -647,7 +672,7 @@ struct HCache {
 template <int NSRC, int NT, bool WRITE>
 __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
                                               const double *htab, double *out, int n_rt,
-                                              int lane, int rows, int kc) {
+                                              int lane, int rows, int kc, ExpTab ex) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
   const ColWalk cw(n, lane);
@@ -670,8 +695,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       const double bx = m.g[g].k.b * xd;
       const double q0 = (m.g[g].k.a * (xd * xd) + bx * yd) + c * (yd * yd);
       const double d0 = bx * S + (c * S) * (2.0 * yd + S);
-      av[g] = m.g[g].amp * exp(-(q0 - cs * (kcd * (kcd + 1.0))));
-      rho[g] = exp(-(d0 + 2.0 * cs * kcd));
+      av[g] = m.g[g].amp * ex(-(q0 - cs * (kcd * (kcd + 1.0))));
+      rho[g] = ex(-(d0 + 2.0 * cs * kcd));
       __builtin_amdgcn_sched_barrier(0);
     }
     const int jj = act ? j : 0;
@@ -737,7 +762,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 template <int NSRC, int NT, bool WRITE, bool FAST>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane,
-                                        HCache *hc = nullptr) {
+                                        const double *etab, HCache *hc = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
@@ -759,23 +784,23 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       const int tw = 2 * rows0;                            // doubles per slot
       const double *h;
       if (!hc) {
-        build_htab<NSRC>(m, vtab, vtab, 3, rows0, kc, (double)cw.S, lane);
+        build_htab<NSRC>(m, vtab, vtab, 3, rows0, kc, (double)cw.S, lane, ExpTab{etab});
         h = vtab;
       } else if (hc->grp == 0) {
         if (!hc->valid) {
-          build_htab<NSRC>(m, vtab + hc->cur * tw, vtab, 3, rows0, kc, (double)cw.S, lane);
+          build_htab<NSRC>(m, vtab + hc->cur * tw, vtab, 3, rows0, kc, (double)cw.S, lane, ExpTab{etab});
           hc->valid = true;
         }
         h = vtab + hc->cur * tw;
       } else {
         double *dst = vtab + (hc->cur ^ 1) * tw;
         build_htab<NSRC>(m, dst, vtab + hc->cur * tw, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3,
-                         rows0, kc, (double)cw.S, lane);
+                         rows0, kc, (double)cw.S, lane, ExpTab{etab});
         hc->flip = true;
         h = dst;
       }
       asm volatile("" ::: "memory");
-      return sweep_fast3<NSRC, NT, WRITE>(m, img, h, out, n, lane, rows, kc);
+      return sweep_fast3<NSRC, NT, WRITE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
     }
     const int lvl = fast_level<NSRC>(m, nn);
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
