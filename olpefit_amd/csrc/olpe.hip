@@ -181,24 +181,29 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     ndone = __builtin_amdgcn_readfirstlane(ndone);
   }
 
-  // chain rows: the next count that records (count >= burn_in, (count - burn_in) %
-  // stride == 0) and its row, advanced by addition (no 64-bit division per step)
-  long long rec_next = -1, rec_row = 0;
+  // chain rows: the iteration (0-based, this launch) of the next record -- count =
+  // count0 + it + 1 >= burn_in and (count - burn_in) % stride == 0 -- and its row,
+  // advanced by 32-bit addition (host: n_iters < 2^31)
+  const int niter = (int)A.n_iters;
+  const int rstride = (int)A.stride;
+  const int nrows = (int)A.nrows;
+  int rec_it = -1, rec_row = 0;
   if (A.stride > 0) {
     const long long c1 = A.count0 + 1;
     const long long k = c1 > A.burn_in ? (c1 - A.burn_in + A.stride - 1) / A.stride : 0;
-    rec_next = A.burn_in + k * A.stride;
-    rec_row = k - A.row0;
+    const long long first = A.burn_in + k * A.stride - c1;
+    rec_it = first < niter ? (int)first : -1;
+    rec_row = (int)(k - A.row0);
   }
+  double *chain_w = A.chain + (size_t)w * A.nrows * PS;
 
   HCache hcache;
   __builtin_amdgcn_s_setprio(1);
-  long long count = A.count0;
 #ifdef OLPE_DIAG_TIMING
   unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long dt_last = __builtin_amdgcn_s_memtime();
 #endif
-  for (long long it = 0; it < A.n_iters; ++it) {
+  for (int it = 0; it < niter; ++it) {
     // randint(0, NP)  (apf_step2.py:302)
     const int r = __builtin_amdgcn_readfirstlane(mt.template randint<NP>(lane));
     // total_tries[rand] += 1  (:304)
@@ -280,8 +285,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
       }
     }
     wave_sync();
-    ++count;
-    if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = count;
+    if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
     DT_MARK(5);
 
 #ifndef OLPE_DIAG_TIMING
@@ -296,10 +300,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     }
 #endif
     // chain record (:342-351, generalised to a stride)
-    if (count == rec_next) {
-      if (rec_row >= 0 && rec_row < A.nrows && lane < PS)
-        A.chain[((size_t)w * A.nrows + rec_row) * PS + lane] = st[lane];
-      rec_next += A.stride;
+    if (it == rec_it) {
+      if (rec_row >= 0 && rec_row < nrows && lane < PS) chain_w[rec_row * PS + lane] = st[lane];
+      rec_it += rstride;
       ++rec_row;
     }
     DT_MARK(6);
@@ -769,6 +772,8 @@ int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_strid
   if (!c->d_state || !c->seeded) return set_err(OLPE_ESTATE, "call olpe_seed first");
   if (n_iters < 0 || burn_in < 0 || record_stride < 0 || accept_min < 0)
     return set_err(OLPE_EINVAL, "negative argument");
+  if (n_iters > 0x7fffffffLL)
+    return set_err(OLPE_EINVAL, "n_iters per launch must be < 2^31 (split the run)");
   HIPCHK(hipSetDevice(c->device));
   // rows recorded in (count0, count0 + n_iters]
   long long row0 = 0, nrows = 0;

@@ -718,7 +718,10 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         acc = act ? fma(t, t, acc) : acc;
       }
     };
-    constexpr int BLK = 4;
+#ifndef OLPE_F3_BLK
+#define OLPE_F3_BLK 4
+#endif
+    constexpr int BLK = OLPE_F3_BLK;
     if (!WRITE && NT != 0 && rows % BLK == 0) {
       const int rstep = cw.S * n;
       const double2 *p = DW + cw.grp * n + jj;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build libolpe.so of a git revision into diag/<name>/ for same-box A/B runs
+# (tools/ab_libs.sh <name>).  usage: tools/build_rev.sh <rev> <name> [extra hipcc flags]
+rev=$1; name=$2; shift 2
+tmp=$(mktemp -d)
+mkdir -p $tmp/olpefit_amd/csrc $tmp/include
+for f in $(git ls-tree --name-only -r $rev olpefit_amd/csrc include); do git show $rev:$f > $tmp/$f; done
+mkdir -p diag/$name
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off "$@" \
+  -o diag/$name/libolpe.so $tmp/olpefit_amd/csrc/olpe.hip $tmp/olpefit_amd/csrc/olpe_comm.hip -lrccl
+rm -rf $tmp
