@@ -57,14 +57,18 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
            background + 3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel G
            multiplies + G-2 adds + 2 fma (the two shape tables, background folded in)
-           + 2 fma (residual, accumulate); per Gaussian and column 2 table exps
-           (E_TAB = 12) + 10 ops; the shape tables are cached across steps and rebuilt
-           for one set (one exp + 3 ops per row) on the 6 of 16 parameter draws that
-           change a shape."""
+           + 2 fma (residual, accumulate); column terms (2 table exps, E_TAB = 12, + 10
+           ops per column) only for the Gaussians the drawn parameter changes -- 12 of
+           the 16 (19) parameters change 2 (NSRC) Gaussians, the rest none -- the other
+           terms are cached (the refresh after an accept is not counted); shape tables
+           rebuilt for one set (one exp + 3 ops per row) on the 6 draws that change one."""
     g = 2 * nsrc
     if mode == "exact":
         return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
-    return n * n * (2 * g + 2) + n * g * (2 * EXP_TAB_OPS + 10) + n * (EXP_TAB_OPS + 3) * 6 / 16
+    np_ = 16 if nsrc == 2 else 19
+    changed = (12 * 2 if nsrc == 2 else (6 * 2 + 2 * 3 + 6 * 3)) / np_
+    return (n * n * (2 * g + 2) + n * changed * (2 * EXP_TAB_OPS + 10)
+            + n * (EXP_TAB_OPS + 3) * 6 / np_)
 
 
 def sec8d_work(n: int, nsrc: int) -> float:

@@ -198,6 +198,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   double *chain_w = A.chain + (size_t)w * A.nrows * PS;
 
   HCache hcache;
+  ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
   __builtin_amdgcn_s_setprio(1);
 #ifdef OLPE_DIAG_TIMING
   unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -260,8 +261,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     // priority so that it is not queued behind the other waves' sweeps
     __builtin_amdgcn_s_setprio(0);
     hcache.grp = grp;
-    const double part =
-        sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab, &hcache);
+    const unsigned gmask = gauss_mask<NSRC>(r);
+    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab,
+                                                     &hcache, &ccache, gmask);
     __builtin_amdgcn_s_setprio(1);
     DT_MARK(3);
     const double chi = wave_sum(part);
@@ -272,6 +274,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     const double dice = mt.rand53(lane);
     const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
     hcache.after(acc);
+    if constexpr (FAST && NT != 0 && NT <= 64) {
+      if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
+    }
     wave_sync();
     if (acc && lane == 0) {
       s_acc[r] = s_acc[r] + 1u;

@@ -669,10 +669,53 @@ struct HCache {
   }
 };
 
-template <int NSRC, int NT, bool WRITE>
+// FAST3 per-column terms of Gaussian q at column xj, row-group offset yr:
+// E = exp(-(Q_0 - c S^2 kc (kc+1))) (a_0 = amp E) and rho.
+struct ColTerm {
+  double E, R;
+};
+__device__ __forceinline__ ColTerm col_term(const Gauss &q, double xj, double yr, double S,
+                                            double kcd, ExpTab ex) {
+  const double xd = xj - q.x0;
+  const double yd = yr - q.y0;
+  const double c = q.k.c;
+  const double cs = c * (S * S);
+  const double bx = q.k.b * xd;
+  const double q0 = (q.k.a * (xd * xd) + bx * yd) + c * (yd * yd);
+  const double d0 = bx * S + (c * S) * (2.0 * yd + S);
+  return ColTerm{ex(-(q0 - cs * (kcd * (kcd + 1.0)))), ex(-(d0 + 2.0 * cs * kcd))};
+}
+
+// Gaussians whose column terms a proposal of parameter r changes (bit g): a source's
+// position moves its two Gaussians, DX/DY the wide ones, a shape set its own; the
+// amplitudes, ratio, offset and background change no E or rho.
+template <int NSRC> __device__ __forceinline__ unsigned gauss_mask(int r) {
+  using L = Layout<NSRC>;
+  unsigned msk = 0;
+#pragma unroll
+  for (int s = 0; s < NSRC; ++s) {
+    if (r == L::sx(s) || r == L::sy(s)) msk |= 3u << (2 * s);
+    if (r == L::DX || r == L::DY || r == L::S2X || r == L::S2Y || r == L::T2) msk |= 1u << (2 * s);
+    if (r == L::S1X || r == L::S1Y || r == L::T1) msk |= 2u << (2 * s);
+  }
+  return msk;
+}
+
+// Per-walker cache (registers) of the current state's FAST3 column terms, for
+// single-pass sweeps (n <= 64): a step recomputes only the Gaussians its proposal
+// changes, and an accepted step refreshes those from the new state.  Cached values are
+// the same pure function of the Gaussian, so results do not depend on the cache.
+template <int G> struct ColCache {
+  double E[G], R[G];
+  unsigned valid = 0;
+};
+
+template <int NSRC, int NT, bool WRITE, bool CC = false>
 __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
                                               const double *htab, double *out, int n_rt,
-                                              int lane, int rows, int kc, ExpTab ex) {
+                                              int lane, int rows, int kc, ExpTab ex,
+                                              ColCache<2 * NSRC> *cc = nullptr,
+                                              unsigned gmask = 0) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
   const ColWalk cw(n, lane);
@@ -688,15 +731,24 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     double av[G], rho[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const double xd = xj - m.g[g].x0;
-      const double yd = yr - m.g[g].y0;
-      const double c = m.g[g].k.c;
-      const double cs = c * (S * S);
-      const double bx = m.g[g].k.b * xd;
-      const double q0 = (m.g[g].k.a * (xd * xd) + bx * yd) + c * (yd * yd);
-      const double d0 = bx * S + (c * S) * (2.0 * yd + S);
-      av[g] = m.g[g].amp * ex(-(q0 - cs * (kcd * (kcd + 1.0))));
-      rho[g] = ex(-(d0 + 2.0 * cs * kcd));
+      ColTerm t;
+      if constexpr (CC) {
+        const bool mine = (gmask >> g) & 1u;
+        if (((cc->valid >> g) & 1u) && !mine) {
+          t = ColTerm{cc->E[g], cc->R[g]};
+        } else {
+          t = col_term(m.g[g], xj, yr, S, kcd, ex);
+          if (!mine) {           // unchanged by the proposal: a term of the current state
+            cc->E[g] = t.E;
+            cc->R[g] = t.R;
+            cc->valid |= 1u << g;
+          }
+        }
+      } else {
+        t = col_term(m.g[g], xj, yr, S, kcd, ex);
+      }
+      av[g] = m.g[g].amp * t.E;
+      rho[g] = t.R;
       __builtin_amdgcn_sched_barrier(0);
     }
     const int jj = act ? j : 0;
@@ -762,10 +814,31 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 
 // FAST kernels keep the exact sweep only as the (rare) fallback, unrolled once so
 // that it does not set the kernel's register budget.
+// After an accepted step: refresh the cached column terms of the Gaussians the step
+// changed from the new state's descriptor.
+template <int NSRC, int NT>
+__device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const ModelDesc<NSRC> &m,
+                                                unsigned gmask, int lane, const double *etab) {
+  const ColWalk cw(NT, lane);
+  const int rows0 = (NT + cw.S - 1) / cw.S;
+  const double kcd = (double)(rows0 / 2);
+#pragma unroll
+  for (int g = 0; g < 2 * NSRC; ++g) {
+    if ((gmask >> g) & 1u) {
+      const ColTerm t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S, kcd,
+                                 ExpTab{etab});
+      cc.E[g] = t.E;
+      cc.R[g] = t.R;
+      cc.valid |= 1u << g;
+    }
+  }
+}
+
 template <int NSRC, int NT, bool WRITE, bool FAST>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane,
-                                        const double *etab, HCache *hc = nullptr) {
+                                        const double *etab, HCache *hc = nullptr,
+                                        ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
@@ -803,6 +876,11 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
         h = dst;
       }
       asm volatile("" ::: "memory");
+      if constexpr (NT != 0 && NT <= 64) {
+        if (cc)
+          return sweep_fast3<NSRC, NT, WRITE, true>(m, img, h, out, n, lane, rows, kc,
+                                                    ExpTab{etab}, cc, gmask);
+      }
       return sweep_fast3<NSRC, NT, WRITE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
     }
     const int lvl = fast_level<NSRC>(m, nn);
