@@ -67,6 +67,8 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
         return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
     np_ = 16 if nsrc == 2 else 19
     changed = (12 * 2 if nsrc == 2 else (6 * 2 + 2 * 3 + 6 * 3)) / np_
+    if n > 64:                       # two column passes: no column-term cache
+        changed = g
     return (n * n * (2 * g + 2) + n * changed * (2 * EXP_TAB_OPS + 10)
             + n * (EXP_TAB_OPS + 3) * 6 / np_)
 
