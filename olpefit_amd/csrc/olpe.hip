@@ -270,7 +270,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     DT_MARK(4);
 
     // accept_reject (:139-148)
-    const double p_accept = exp(-(chi - st[PS - 1]) / 2.);
+    // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
+    const double la = -(chi - st[PS - 1]) / 2.;
+    const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
     const double dice = mt.rand53(lane);
     const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
     hcache.after(acc);
