@@ -11,13 +11,18 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libolpe.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("olpe.hip", "olpe_comm.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("olpe_device.h", "olpe_internal.h")] + [
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("olpe_device.h", "olpe_internal.h",
+                                                 "exp_table.h")] + [
     os.path.join(REPO, "include", "olpe.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          # numpy evaluates a*b + c as two rounded ops; keep that order in the
          # control path and the per-pixel expression (fma only where written)
          "-ffp-contract=off",
+         # MachineLICM hoists the loop's FP64 constants (ocml polynomial coefficients,
+         # LDS slice addresses) out of the sampler loop into registers and then spills
+         # them: without it the sampler kernel has no spills (+5 % fast, +6 % 3-source)
+         "-mllvm", "-disable-machine-licm",
          "-Wall", "-Wno-unused-function"]
 
 
@@ -41,4 +46,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--print-flags" in sys.argv:      # for tools/diag_build.sh and tools/build_rev.sh
+        print(" ".join(f for f in FLAGS if f not in ("-Wall", "-Wno-unused-function")))
+    else:
+        build(force="--force" in sys.argv)

@@ -6,6 +6,6 @@ tmp=$(mktemp -d)
 mkdir -p $tmp/olpefit_amd/csrc $tmp/include
 for f in $(git ls-tree --name-only -r $rev olpefit_amd/csrc include); do git show $rev:$f > $tmp/$f; done
 mkdir -p diag/$name
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off "$@" \
+/opt/rocm/bin/hipcc $(python -m olpefit_amd.build --print-flags) "$@" \
   -o diag/$name/libolpe.so $tmp/olpefit_amd/csrc/olpe.hip $tmp/olpefit_amd/csrc/olpe_comm.hip -lrccl
 rm -rf $tmp

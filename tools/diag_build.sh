@@ -3,5 +3,5 @@
 # product library).  usage: tools/diag_build.sh <name> <extra hipcc flags...>
 name=$1; shift
 mkdir -p diag/$name
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off \
+/opt/rocm/bin/hipcc $(python -m olpefit_amd.build --print-flags) \
   "$@" -o diag/$name/libolpe.so olpefit_amd/csrc/olpe.hip olpefit_amd/csrc/olpe_comm.hip -lrccl
