@@ -247,11 +247,23 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     } else {
       C2p = ld_coef(st + WS::OC2);
     }
-    // the step's model descriptor goes to LDS: the sweep loads each field where it
-    // is used instead of holding 6*G doubles in registers across it
-    {
-      const ModelDesc<NSRC> md = make_model<NSRC>(q, C1p, C2p, A.bkgd_mode);
-      if (lane == 0) *mdl = md;
+    // the step's model descriptor goes to LDS (the sweep loads each field where it is
+    // used instead of holding 6*G doubles in registers across it), built lane-parallel:
+    // lane g < G writes Gaussian g with make_model's operations, lane G the background
+    if (lane < 2 * NSRC) {
+      const int s = lane >> 1;
+      const bool narrow = lane & 1;
+      auto ql = [&](int k) -> double { return (k == r) ? nv : st[k]; };
+      const double tot = ql(L::sa(s)) - ql(L::OFF);
+      const double wide = tot * ql(L::RATIO);
+      const double xc = ql(L::sx(s)), yc = ql(L::sy(s));
+      // component-wise selects (a select of whole structs goes through scratch)
+      const Coef C{narrow ? C1p.a : C2p.a, narrow ? C1p.b : C2p.b, narrow ? C1p.c : C2p.c};
+      const double dx = narrow ? 0.0 : ql(L::DX), dy = narrow ? 0.0 : ql(L::DY);
+      mdl->g[lane] = Gauss{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
+                           narrow ? yc : yc + dy, C};
+    } else if (lane == 2 * NSRC) {
+      mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
     }
     wave_sync();
     DT_MARK(2);
