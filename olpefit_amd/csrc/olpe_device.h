@@ -208,12 +208,15 @@ __device__ inline void mt_seed_serial(uint32_t *key, uint32_t s) {
 // exp(x) for the FAST3 setup (guarded arguments): x = (64 k + j) ln2/64 + r with
 // |r| <= ln2/128, exp(x) = 2^k * T[j] * (1 + q(r)), q of degree 5, T = 2^(j/64) from an
 // LDS copy of c_exp2_64.  12 FP64 operations instead of ocml's 19 plus range selects;
-// <= 1.13 ulp (tools/gen_exp_table.py --check).  Arguments are clamped to [-745, 709].
+// <= 1.13 ulp (tools/gen_exp_table.py --check).  Arguments are clamped to [-1000, 710]
+// (underflow to 0, overflow to inf); NaN is not propagated (callers are guarded).
+// (A {hi, lo}-table, degree-6 variant reaches 0.51 ulp but, with its LDS gather in the
+// dependency chain, ran the EXACT sweep 13 % slower than ocml's exp: not used.)
 constexpr int kEtabBytes = 64 * 8;
 struct ExpTab {
   const double *T;
   __device__ __forceinline__ double operator()(double x) const {
-    x = fmin(fmax(x, -745.0), 709.0);
+    x = fmin(fmax(x, -1000.0), 710.0);
     const double kd = __builtin_rint(x * kExpInv);
     double r = fma(-kd, kExpHi, x);
     r = fma(-kd, kExpLo, r);
