@@ -216,7 +216,11 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
 
     // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
     const double cur = uniform_f64(st[r]);
+#ifdef OLPE_DIAG_NO_GAUSS
+    const double g = 0.01 * (double)(r - 8);      // diagnostic: no polar draw
+#else
     const double g = mt.gauss_next(lane);
+#endif
     const double wr = width_of<NSRC>(r);
     double nv;
     if ((L::LOGMASK >> r) & 1u) {
@@ -311,7 +315,9 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
     hcache.after(acc);
     if constexpr (FAST && NT != 0 && NT <= 64) {
+#ifndef OLPE_DIAG_NO_REFRESH
       if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
+#endif
     }
     wave_sync();
     if (acc && lane == 0) {
@@ -349,8 +355,8 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     DT_MARK(6);
   }
 #ifdef OLPE_DIAG_TIMING
-  if (A.trace && lane < 7) {
-    unsigned long long v = 0;
+  if (A.trace && lane < 9) {
+    unsigned long long v = lane == 7 ? ccache.n_setup : lane == 8 ? ccache.n_refresh : 0;
     for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
     A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
   }

@@ -711,6 +711,9 @@ template <int NSRC> __device__ __forceinline__ unsigned gauss_mask(int r) {
 template <int G> struct ColCache {
   double E[G], R[G];
   unsigned valid = 0;
+#ifdef OLPE_DIAG_TIMING
+  unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
+#endif
 };
 
 template <int NSRC, int NT, bool WRITE, bool CC = false>
@@ -737,10 +740,17 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       ColTerm t;
       if constexpr (CC) {
         const bool mine = (gmask >> g) & 1u;
+#ifdef OLPE_DIAG_NO_COLTERM
+        if (true) {                              // diagnostic: column terms never recomputed
+#else
         if (((cc->valid >> g) & 1u) && !mine) {
+#endif
           t = ColTerm{cc->E[g], cc->R[g]};
         } else {
           t = col_term(m.g[g], xj, yr, S, kcd, ex);
+#ifdef OLPE_DIAG_TIMING
+          ++cc->n_setup;
+#endif
           if (!mine) {           // unchanged by the proposal: a term of the current state
             cc->E[g] = t.E;
             cc->R[g] = t.R;
@@ -832,6 +842,9 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
 #pragma unroll
   for (int g = 0; g < 2 * NSRC; ++g) {
     if ((gmask >> g) & 1u) {
+#ifdef OLPE_DIAG_TIMING
+      ++cc.n_refresh;
+#endif
       const ColTerm t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S, kcd,
                                  ExpTab{etab});
       cc.E[g] = t.E;
@@ -861,7 +874,11 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     const int rows = (nn - cw.grp + cw.S - 1) / cw.S;    // uniform when S divides n
     const int rows0 = (nn + cw.S - 1) / cw.S;             // rows of row group 0 (most)
     const int kc = rows0 / 2;
+#ifdef OLPE_DIAG_NO_GUARD
+    const bool ok3 = true;                       // diagnostic: guard skipped
+#else
     const bool ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+#endif
     asm volatile("" ::: "memory");
     if (ok3) {
       const int tw = 2 * rows0;                            // doubles per slot

@@ -39,7 +39,10 @@ def main():
     s.run(iters, burn_in=0, record_stride=10)
     wall = time.perf_counter() - t0
     kms = s.last_kernel_ms()
-    tr = s.trace(iters).reshape(W, -1)[:, :7] / iters              # cycles per step, per walker
+    full = s.trace(iters).reshape(W, -1)
+    tr = full[:, :7] / iters                           # ticks per step, per walker
+    print(f"column terms per step: setup {full[:, 7].mean() / iters:.3f}, "
+          f"refresh after accept {full[:, 8].mean() / iters:.3f}")
     tot = tr.sum(axis=1)
     print(f"walkers {W} iters {iters} kernel {kms:.2f} ms (wall {wall * 1e3:.1f} ms)")
     print(f"per-wave step total: mean {tot.mean():.0f} ticks (min {tot.min():.0f}, "
