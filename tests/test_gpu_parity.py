@@ -196,6 +196,27 @@ def test_long_run_matches_oracle(golden, lib_loaded, mode):
     assert np.all(np.isfinite(pos))
 
 
+def test_long_run_64_fast_matches_oracle(golden, lib_loaded):
+    """64x64 (the unrolled FAST3 row loop, the column-term and shape-table caches,
+    accepts refreshing the caches): 2 walkers x 2500 iterations against the oracle."""
+    g = golden("c64")
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    seeds = [21, 22]
+    n_it = 2500
+    s = make_sampler(g, "fast")
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (2, 1)))
+    s.enable_trace(True)
+    chain = s.run(n_it, burn_in=0, record_stride=1)
+    tr = s.trace(n_it)
+    for w, sd in enumerate(seeds):
+        ref_chain, ref_tr = ora.Walker(dm, err, g["p_init"], sd).run(n_it, trace=True)
+        np.testing.assert_allclose(chain[w], ref_chain, rtol=10 * TOL["fast"]["traj"],
+                                   atol=1e-9)
+        assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in ref_tr], bool))
+    assert 0.05 < tr[:, :, 5].mean() < 0.95          # both outcomes exercised
+
+
 def test_negative_log_parameter_is_always_rejected(golden, lib_loaded):
     """A log-normal parameter <= 0 proposes NaN (log10), which the reference always
     rejects (NaN chi^2 / masked sum, apf_step2.py:144); same trajectory as the oracle."""
