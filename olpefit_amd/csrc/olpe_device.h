@@ -630,8 +630,10 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
   const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
   const double Qb = (q.k.a * (mx * mx) + fabs(q.k.b) * mx * my) + q.k.c * (my * my);
   const double cs = q.k.c * S2;
-  const bool ok = (cs * km * km < 600.0) && (Qb < 700.0 + cs * kc * (kc + 1.0)) &&
-                  isfinite(Qb) && isfinite(q.amp) && (q.k.a >= 0.0) && (q.k.c >= 0.0);
+  // bitwise &: no short-circuit branches (exec-mask juggling) in the lane-parallel test
+  const bool ok = (int)(cs * km * km < 600.0) & (int)(Qb < 700.0 + cs * kc * (kc + 1.0)) &
+                  (int)isfinite(Qb) & (int)isfinite(q.amp) & (int)(q.k.a >= 0.0) &
+                  (int)(q.k.c >= 0.0);
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
