@@ -55,9 +55,10 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
 
     exact: per pixel-Gaussian 7 ops + one exp (E = 20), per pixel G-1 combines +
            background + 3 residual ops, per column-Gaussian 4 hoisted ops.
-    fast:  the FAST3 sweep every guarded step of this workload takes: per pixel G
-           multiplies + G-2 adds + 2 fma (the two shape tables, background folded in)
-           + 2 fma (residual, accumulate); column terms (2 table exps, E_TAB = 12, + 10
+    fast:  the FAST3 sweep every guarded step of this workload takes: per pixel, with
+           the four-row update, 2 sets x (5m-1)/4 (m = nsrc Gaussians per set; G
+           multiplies + G-2 adds per pixel without it) + 2 fma (the two shape tables,
+           background folded in) + 2 fma (residual, accumulate); column terms (2 table exps, E_TAB = 12, + 10
            ops per column) only for the Gaussians the drawn parameter changes -- 12 of
            the 16 (19) parameters change 2 (NSRC) Gaussians, the rest none -- the other
            terms are cached (the refresh after an accept is not counted); shape tables
@@ -69,7 +70,9 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
     changed = (12 * 2 if nsrc == 2 else (6 * 2 + 2 * 3 + 6 * 3)) / np_
     if n > 64:                       # two column passes: no column-term cache
         changed = g
-    return (n * n * (2 * g + 2) + n * changed * (2 * EXP_TAB_OPS + 10)
+    # four-row update (n >= 64): 2 sets x (5m - 1)/4 + 4 per pixel, m = nsrc per set
+    per_px = (5 * nsrc - 1) / 2 + 4 if n >= 64 else 2 * g + 2
+    return (n * n * per_px + n * changed * (2 * EXP_TAB_OPS + 10)
             + n * (EXP_TAB_OPS + 3) * 6 / np_)
 
 
