@@ -86,10 +86,11 @@ constexpr int kTraceF = 6;
 // ---------------------------------------------------------------------------------
 // The fused sampler
 // ---------------------------------------------------------------------------------
-// Per-wave LDS slice: MT key[624] | tries[NP] | accepts[NP] | state doubles (below)
-// | per-step model descriptor | (after BYTES) the V table of sweep_fast
+// Per-wave LDS slice: tries[NP] | accepts[NP] | state doubles (below) | per-step model
+// descriptor | the proposal's column terms of the Gaussians it moves (E, rho per lane,
+// NSRC slots) | (after BYTES) the shape tables / V table.  The MT key stays in HBM.
 template <int NP> struct WaveSlice {
-  static constexpr int U32 = MT_N + 2 * NP;                  // 8-byte multiple for NP 16/19
+  static constexpr int U32 = 2 * NP;                         // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
   static constexpr int NSRC = NP == 16 ? 2 : 3;
   // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
@@ -97,7 +98,8 @@ template <int NP> struct WaveSlice {
   static constexpr int OPT = PS + 12, OPC = PS + 15;
   static constexpr int F64 = PS + 18;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
-  static constexpr int BYTES = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
+  static constexpr int OPE = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
+  static constexpr int BYTES = OPE + NSRC * 2 * 64 * 8;
 };
 // bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
 __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
@@ -130,8 +132,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   const int wstride = WS::BYTES + vtab_bytes(n, NSRC);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (size_t)wave * wstride;
-  uint32_t *key = reinterpret_cast<uint32_t *>(wb);
-  uint32_t *s_tries = key + MT_N;
+  uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
   double *vtab = reinterpret_cast<double *>(wb + WS::BYTES);
@@ -149,7 +150,6 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   if (w >= A.W) return;
 
   // ---- walker state -> LDS slice
-  for (int k = lane; k < MT_N; k += 64) key[k] = A.mt[w * MT_N + k];
   if (lane < NP) {
     s_tries[lane] = A.tries[w * NP + lane];
     s_acc[lane] = A.accepts[w * NP + lane];
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
   wave_sync();
 
   MTWave mt;
-  mt.key = key;
+  mt.key = A.mt + (size_t)w * MT_N;
   mt.pos = __builtin_amdgcn_readfirstlane(A.mt_pos[w]);
   mt.bstart = mt.pos;
   mt.bsize = 0;
@@ -199,6 +199,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
 
   HCache hcache;
   ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
+  ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
   __builtin_amdgcn_s_setprio(1);
 #ifdef OLPE_DIAG_TIMING
   unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -318,6 +319,7 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
 #ifndef OLPE_DIAG_NO_REFRESH
       if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
 #endif
+      ccache.pend = 0;              // parked terms belong to this step only
     }
     wave_sync();
     if (acc && lane == 0) {
@@ -369,7 +371,6 @@ __global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
     A.tries[w * NP + lane] = s_tries[lane];
     A.accepts[w * NP + lane] = s_acc[lane];
   }
-  for (int k = lane; k < MT_N; k += 64) A.mt[w * MT_N + k] = key[k];
   if (lane == 0) {
     A.mt_pos[w] = mt.pos;
     A.has_gauss[w] = mt.has_gauss;
@@ -437,14 +438,11 @@ template <int NP>
 __global__ __launch_bounds__(64) void olpe_stream_kernel(uint32_t *mtg, int *posg,
                                                          int *hasg, double *gg, int W,
                                                          int kind, int nd, void *out) {
-  __shared__ uint32_t key[MT_N];
   const int lane = threadIdx.x;
   const int w = blockIdx.x;
   if (w >= W) return;
-  for (int k = lane; k < MT_N; k += 64) key[k] = mtg[(size_t)w * MT_N + k];
-  wave_sync();
   MTWave mt;
-  mt.key = key;
+  mt.key = mtg + (size_t)w * MT_N;
   mt.pos = __builtin_amdgcn_readfirstlane(posg[w]);
   mt.bstart = mt.pos;
   mt.bsize = 0;
@@ -463,8 +461,6 @@ __global__ __launch_bounds__(64) void olpe_stream_kernel(uint32_t *mtg, int *pos
       if (lane == 0) reinterpret_cast<double *>(out)[(size_t)w * nd + i] = v;
     }
   }
-  wave_sync();
-  for (int k = lane; k < MT_N; k += 64) mtg[(size_t)w * MT_N + k] = key[k];
   if (lane == 0) {
     posg[w] = mt.pos;
     hasg[w] = mt.has_gauss;

@@ -99,35 +99,72 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// numpy mt19937_gen, parallelised over 64 lanes.  Pass [i0, i0+64) writes key[i] and
-// reads key[i] / key[i+1] (old) and key[i+397] (old, i < 227) or key[i-227] (new,
-// written by an EARLIER pass since 227 > 64); so 10 ordered passes + the last word
-// reproduce the sequential update exactly.
-__device__ inline void mt_twist(uint32_t *key, int lane) {
-  for (int i0 = 0; i0 < MT_N - 1; i0 += 64) {
-    const int i = i0 + lane;
-    uint32_t ki = 0, ki1 = 0, src = 0;
-    if (i < MT_N - 1) {
-      ki = key[i];
-      ki1 = key[i + 1];
-      src = (i < MT_N - MT_M) ? key[i + MT_M] : key[i - (MT_N - MT_M)];
+// The key stays in HBM (one 2,496-B row per walker); it is only touched by a refill
+// of the 64-word batch (every 64 draws) and by the twist (every 624), through
+// agent-scope atomics so that a load sees this wave's earlier stores.
+__device__ __forceinline__ uint32_t key_ld(const uint32_t *k, int i) {
+  return __hip_atomic_load(const_cast<uint32_t *>(k) + i, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void key_st(uint32_t *k, int i, uint32_t v) {
+  __hip_atomic_store(k + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t lane_from(uint32_t v, int src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((src_lane & 63) << 2, (int)v);
+}
+
+// numpy mt19937_gen in registers: lane l holds key[64 p + l] in k[p] (p = 0..9).  Pass
+// p writes key[i], i = 64p + l, from key[i], key[i+1] (old) and key[i+397] (old, i <
+// 227: k[p+6] / k[p+7]) or key[i-227] (new, written by an EARLIER pass since 227 > 64:
+// k[p-4] / k[p-3]); the cross-lane reads are ds_bpermute (no LDS storage).  10 ordered
+// passes + the last word reproduce the sequential update exactly.  Returns the new
+// words 0..63 (lane l: key[l]), the next batch.
+__device__ inline uint32_t mt_twist(uint32_t *gkey, int lane) {
+  uint32_t k[10];
+#pragma unroll
+  for (int p = 0; p < 10; ++p) k[p] = (64 * p + lane < MT_N) ? key_ld(gkey, 64 * p + lane) : 0u;
+#pragma unroll
+  for (int p = 0; p < 10; ++p) {
+    const int i = 64 * p + lane;
+    uint32_t ki1 = lane_from(k[p], lane + 1);                  // key[i+1], lanes 0..62
+    if (p < 9) {
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)k[p + 1], 0);
+      ki1 = lane == 63 ? nx : ki1;
     }
-    wave_sync();
-    if (i < MT_N - 1) {
-      const uint32_t y = (ki & MT_UP) | (ki1 & MT_LO);
-      key[i] = src ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+    // (every ds_bpermute runs with the whole wave active: it reads inactive lanes as 0)
+    uint32_t src = 0;
+    if (p + 6 <= 9) src = lane_from(k[p + 6], lane + 13);     // key[i+397], lanes 0..50
+    if (p + 7 <= 9) {
+      const uint32_t s7 = lane_from(k[p + 7], lane - 51);     // lanes 51..63
+      src = lane > 50 ? s7 : src;
     }
-    wave_sync();
+    if (p >= 3) {                                             // key[i-227] (new)
+      uint32_t nw = 0;
+      if (p >= 4) nw = lane_from(k[p - 4], lane + 29);          // lanes 0..34
+      const uint32_t nw2 = lane_from(k[p - 3], lane - 35);      // lanes 35..63
+      nw = lane > 34 ? nw2 : nw;
+      src = i >= MT_N - MT_M ? nw : src;
+    }
+    const uint32_t y = (k[p] & MT_UP) | (ki1 & MT_LO);
+    const uint32_t nv = src ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+    k[p] = i < MT_N - 1 ? nv : k[p];
   }
-  if (lane == 0) {
-    const uint32_t y = (key[MT_N - 1] & MT_UP) | (key[0] & MT_LO);
-    key[MT_N - 1] = key[MT_M - 1] ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+  {  // the last word, key[623] = key[396] ^ twist(key[623], key[0]) with new key[0, 396]
+    const uint32_t k623 = (uint32_t)__builtin_amdgcn_readlane((int)k[9], 47);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k[0], 0);
+    const uint32_t k396 = (uint32_t)__builtin_amdgcn_readlane((int)k[6], 12);
+    const uint32_t y = (k623 & MT_UP) | (k0 & MT_LO);
+    const uint32_t nv = k396 ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+    k[9] = lane == 47 ? nv : k[9];
   }
-  wave_sync();
+#pragma unroll
+  for (int p = 0; p < 10; ++p)
+    if (64 * p + lane < MT_N) key_st(gkey, 64 * p + lane, k[p]);
+  return k[0];
 }
 
 struct MTWave {
-  uint32_t *key;  // LDS, MT_N words
+  uint32_t *key;  // HBM, MT_N words (this walker's row)
   int pos;        // numpy state->pos (uniform)
   int bstart;     // first key index held in `batch`
   int bsize;      // valid lanes in `batch`
@@ -136,12 +173,15 @@ struct MTWave {
   double gauss;
 
   __device__ void refill(int lane) {
+    uint32_t v;
     if (pos >= MT_N) {
-      mt_twist(key, lane);
+      v = mt_twist(key, lane);
       pos = 0;
+    } else {
+      const int n = (MT_N - pos) < 64 ? (MT_N - pos) : 64;
+      v = (lane < n) ? key_ld(key, pos + lane) : 0u;
     }
     const int n = (MT_N - pos) < 64 ? (MT_N - pos) : 64;
-    const uint32_t v = (lane < n) ? key[pos + lane] : 0u;
     batch = mt_temper(v);
     bstart = pos;
     bsize = n;
@@ -713,6 +753,11 @@ template <int NSRC> __device__ __forceinline__ unsigned gauss_mask(int r) {
 template <int G> struct ColCache {
   double E[G], R[G];
   unsigned valid = 0;
+  // LDS: the proposal's (E, rho) of the Gaussians it moves, [slot][2][64 lanes] with
+  // slot = rank of g among the moved ones; an accept copies them instead of
+  // recomputing (pend = the gmask they belong to)
+  double *pbuf = nullptr;
+  unsigned pend = 0;
 #ifdef OLPE_DIAG_TIMING
   unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
 #endif
@@ -757,6 +802,10 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
             cc->E[g] = t.E;
             cc->R[g] = t.R;
             cc->valid |= 1u << g;
+          } else if (cc->pbuf) { // moved: park the proposal's terms for an accept
+            const int slot = __builtin_popcount(gmask & ((1u << g) - 1u));
+            cc->pbuf[(2 * slot) * 64 + lane] = t.E;
+            cc->pbuf[(2 * slot + 1) * 64 + lane] = t.R;
           }
         }
       } else {
@@ -766,6 +815,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       rho[g] = t.R;
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (CC) cc->pend = gmask;
     const int jj = act ? j : 0;
     const double2 *hr = reinterpret_cast<const double2 *>(htab);
     auto row = [&](int i, double2 h, double2 dw) {
@@ -878,19 +928,27 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
   const ColWalk cw(NT, lane);
   const int rows0 = (NT + cw.S - 1) / cw.S;
   const double kcd = (double)(rows0 / 2);
+  const bool parked = cc.pbuf && cc.pend == gmask;   // this step's FAST3 setup ran
 #pragma unroll
   for (int g = 0; g < 2 * NSRC; ++g) {
     if ((gmask >> g) & 1u) {
+      if (parked) {
+        const int slot = __builtin_popcount(gmask & ((1u << g) - 1u));
+        cc.E[g] = cc.pbuf[(2 * slot) * 64 + lane];
+        cc.R[g] = cc.pbuf[(2 * slot + 1) * 64 + lane];
+      } else {
 #ifdef OLPE_DIAG_TIMING
-      ++cc.n_refresh;
+        ++cc.n_refresh;
 #endif
-      const ColTerm t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S, kcd,
-                                 ExpTab{etab});
-      cc.E[g] = t.E;
-      cc.R[g] = t.R;
+        const ColTerm t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S,
+                                   kcd, ExpTab{etab});
+        cc.E[g] = t.E;
+        cc.R[g] = t.R;
+      }
       cc.valid |= 1u << g;
     }
   }
+  cc.pend = 0;
 }
 
 template <int NSRC, int NT, bool WRITE, bool FAST>
