@@ -115,7 +115,9 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
 }
 
 template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
-__global__ __launch_bounds__(WPB * 64) void olpe_gibbs_kernel(GibbsArgs A) {
+// The global-memory (large cutout) variant runs 4-wave workgroups and waits on L2: it
+// is asked to fit 4 of them per CU (128 VGPRs; 2 waves per SIMD otherwise): +7 %
+__global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
   constexpr int NP = L::NP, PS = L::PS;

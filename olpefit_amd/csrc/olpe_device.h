@@ -654,8 +654,9 @@ __device__ __forceinline__ double sweep_fast2(const ModelDesc<NSRC> &m, const do
 // G_k = a_k * H_k exactly (Q_k is quadratic in k).  a_k is geometric (1 multiply per
 // pixel-Gaussian, <= k ulp), H comes from an LDS table read once per row for all
 // Gaussians:  model = fma(sum_narrow a, H_n, fma(sum_wide a, H_w, bg)).
-// 10 FP64 ops per pixel for 2 sources (FAST2: 14); 8.5 with the four-row update below.  Guard (fast3_ok): c S^2 (kc+1)^2
-// < 600 keeps a_k from overflowing and H from underflowing, and the FAST2 bound on Q
+// 10 FP64 ops per pixel for 2 sources (FAST2: 14); 8.5 with the four-row update below.
+// Guard (fast3_ok): c S^2 (kc+1)^2 < 600 keeps a_k from overflowing and H from
+// underflowing, and the FAST2 bound on Q
 // (relaxed by c S^2 kc (kc+1)) keeps a_0 from underflowing where G is significant.
 // Lane-parallel: lane g < 2*NSRC tests Gaussian g (the descriptor is in LDS), one
 // ballot combines them.
@@ -899,7 +900,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           nxt[k] = pn[k * rstep];
           hn[k] = hr[hb + k];
         }
-        row4(hc, cur);
+#pragma unroll
+        for (int k = 0; k < BLK; k += 4) row4(hc + k, cur + k);
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
           cur[k] = nxt[k];
