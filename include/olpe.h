@@ -97,7 +97,8 @@ int olpe_state_get(olpe_ctx *ctx, double *state, double *tries, double *accepts)
  * device chain buffer of this launch (read with olpe_chain_read).  record_stride 0
  * records nothing.  accept_min > 0 tracks, per walker, the first c at which every
  * parameter has been tried accept_min times (the loop condition :300); read it with
- * olpe_done_at.  *nrec_out (may be NULL) = rows recorded per walker by this launch. */
+ * olpe_done_at.  *nrec_out (may be NULL) = rows recorded per walker by this launch.
+ * n_iters per call must be < 2^31 (OLPE_EINVAL otherwise; split long runs). */
 int olpe_run(olpe_ctx *ctx, long long n_iters, long long burn_in, int record_stride,
              long long accept_min, long long *nrec_out);
 /* Copy the last launch's chain [W][nrec][PS] to the host (synchronises). */
