@@ -101,6 +101,13 @@ template <int NP> struct WaveSlice {
   static constexpr int OPE = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
   static constexpr int BYTES = OPE + NSRC * 2 * 64 * 8;
 };
+// MTWave draw tables (kDrawTab doubles per wave).  Kernels with the FAST3 column-term
+// cache (NT = 32, 64) keep them after the slice; the others in the parking area of
+// the proposal's column terms, which only that cache uses.
+constexpr int kDrawTabBytes = (kDrawTab * 8 + 15) & ~15;
+__host__ __device__ constexpr int drawtab_extra(int nt) {
+  return (nt != 0 && nt <= 64) ? kDrawTabBytes : 0;
+}
 // bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
 __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
@@ -131,13 +138,15 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(G
   // ---- LDS carve: exp table, [DE] (if staged), then one {WaveSlice, V table} per wave
   double *etab = reinterpret_cast<double *>(smem);
   double2 *sDE = reinterpret_cast<double2 *>(smem + kEtabBytes);
-  const int wstride = WS::BYTES + vtab_bytes(n, NSRC);
+  constexpr int TABX = drawtab_extra(NT);
+  const int wstride = WS::BYTES + TABX + vtab_bytes(n, NSRC);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (size_t)wave * wstride;
   uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
-  double *vtab = reinterpret_cast<double *>(wb + WS::BYTES);
+  double *vtab = reinterpret_cast<double *>(wb + WS::BYTES + TABX);
+  double *drawtab = reinterpret_cast<double *>(wb + (TABX ? WS::BYTES : WS::OPE));
   ModelDesc<NSRC> *mdl = reinterpret_cast<ModelDesc<NSRC> *>(wb + WS::OMD);
 
   if constexpr (LDS_IMG) {
@@ -175,6 +184,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(G
   mt.batch = 0;
   mt.has_gauss = __builtin_amdgcn_readfirstlane(A.has_gauss[w]);
   mt.gauss = uniform_f64(A.gauss[w]);
+  mt.tab = drawtab;
 
   int ndone = 0;
   long long done_at = A.done_at[w];
@@ -208,8 +218,18 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(G
   unsigned long long dt_last = __builtin_amdgcn_s_memtime();
 #endif
   for (int it = 0; it < niter; ++it) {
-    // randint(0, NP)  (apf_step2.py:302)
-    const int r = __builtin_amdgcn_readfirstlane(mt.template randint<NP>(lane));
+    // the iteration's draws: randint(0, NP) (apf_step2.py:302), the proposal's gauss()
+    // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
+    int r0 = 0, dice_idx = 0;
+    double g = 0.0;
+#ifdef OLPE_DIAG_NO_GAUSS
+    mt.template draw<NP>(lane, 0, 0, r0, g, dice_idx);
+    mt.template draw<NP>(lane, 2, 2, r0, g, dice_idx);
+    g = 0.01 * (double)(r0 - 8);                  // diagnostic: no polar draw
+#else
+    mt.template draw<NP>(lane, 0, 2, r0, g, dice_idx);
+#endif
+    const int r = __builtin_amdgcn_readfirstlane(r0);
     // total_tries[rand] += 1  (:304)
     const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
     wave_sync();
@@ -219,11 +239,6 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(G
 
     // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
     const double cur = uniform_f64(st[r]);
-#ifdef OLPE_DIAG_NO_GAUSS
-    const double g = 0.01 * (double)(r - 8);      // diagnostic: no polar draw
-#else
-    const double g = mt.gauss_next(lane);
-#endif
     const double wr = width_of<NSRC>(r);
     double nv;
     if ((L::LOGMASK >> r) & 1u) {
@@ -314,7 +329,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(G
     // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
     const double la = -(chi - st[PS - 1]) / 2.;
     const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
-    const double dice = mt.rand53(lane);
+    const double dice = drawtab[dice_idx];
     const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
     hcache.after(acc);
     if constexpr (FAST && NT != 0 && NT <= 64) {
@@ -443,7 +458,9 @@ __global__ __launch_bounds__(64) void olpe_stream_kernel(uint32_t *mtg, int *pos
   const int lane = threadIdx.x;
   const int w = blockIdx.x;
   if (w >= W) return;
+  __shared__ double drawtab[kDrawTab];
   MTWave mt;
+  mt.tab = drawtab;
   mt.key = mtg + (size_t)w * MT_N;
   mt.pos = __builtin_amdgcn_readfirstlane(posg[w]);
   mt.bstart = mt.pos;
@@ -456,10 +473,13 @@ __global__ __launch_bounds__(64) void olpe_stream_kernel(uint32_t *mtg, int *pos
       const uint32_t v = mt.next(lane);
       if (lane == 0) reinterpret_cast<uint32_t *>(out)[(size_t)w * nd + i] = v;
     } else {
-      double v;
-      if (kind == 1) v = mt.rand53(lane);
-      else if (kind == 2) v = mt.gauss_next(lane);
-      else v = (double)mt.template randint<NP>(lane);
+      // the sampler's draw path, one stage at a time
+      int r = 0, di = 0;
+      double v = 0.0;
+      const int stage = kind == 1 ? 2 : kind == 2 ? 1 : 0;
+      mt.template draw<NP>(lane, stage, stage, r, v, di);
+      if (kind == 1) v = drawtab[di];
+      else if (kind == 3) v = (double)r;
       if (lane == 0) reinterpret_cast<double *>(out)[(size_t)w * nd + i] = v;
     }
   }
@@ -513,13 +533,16 @@ template <class T> int dev_alloc(T **p, size_t count) {
   return OLPE_OK;
 }
 
-size_t wave_lds(int n, int np) {
-  return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) +
+// per-wave LDS of the kernel launch_gibbs_m picks: NT = n for LDS images of 32 and 64
+// pixels, otherwise NT = 0 / 128 (no extra draw-table bytes)
+size_t wave_lds(int n, int np, bool lds_img) {
+  const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
+  return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
          vtab_bytes(n, np == 16 ? 2 : 3);
 }
 
 size_t lds_bytes(const olpe_ctx *c, int wpb) {
-  size_t b = (size_t)wpb * wave_lds(c->n, c->np) + kEtabBytes;
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img) + kEtabBytes;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   return b;
 }
@@ -632,7 +655,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->ps = c->np + 1;
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
-  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np) + kEtabBytes <= 160 * 1024;
+  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np, true) + kEtabBytes <= 160 * 1024;
   if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
   std::vector<double2> hDE(npix), hDW(npix);

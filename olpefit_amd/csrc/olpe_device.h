@@ -84,9 +84,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // ---------------------------------------------------------------------------------
 // MT19937 + NumPy legacy distributions
-// The 624-word key lives in LDS (one slice per wave).  Draws are wave-uniform: a
-// batch of 64 tempered outputs is held one-per-lane in a VGPR and read out with
-// v_readlane, so a draw costs one VALU op plus scalar bookkeeping.
+// Draws are wave-uniform: a batch of 64 tempered outputs is held one-per-lane in a
+// VGPR and read out with v_readlane, so a raw draw costs one VALU op plus scalar
+// bookkeeping.  The floating-point draws are prepared lane-parallel once per batch
+// (MTWave::prep): lane l computes rand() of words (l, l+1) and the whole polar
+// attempt starting at word l (acceptance bit, factor sqrt(-2 log r2 / r2)), so a
+// rand() or a gauss() whose words lie in the batch is a table read instead of ~100
+// wave-uniform FP64 instructions; draws straddling the batch end take the scalar path.
 // ---------------------------------------------------------------------------------
 constexpr int MT_N = 624, MT_M = 397;
 constexpr uint32_t MT_A = 0x9908b0dfu, MT_UP = 0x80000000u, MT_LO = 0x7fffffffu;
@@ -171,7 +175,14 @@ struct MTWave {
   uint32_t batch; // tempered key[bstart + lane]
   int has_gauss;
   double gauss;
+  // per-batch draw tables (LDS, kDrawTab doubles per wave): tab[l] = rand() of words
+  // (l, l+1), tab[64 + l] = polar factor sqrt(-2 log r2 / r2) of the attempt at word
+  // l, or -1 where that attempt is rejected (l + 3 < bsize), tab[128] = a rand()
+  // assembled across the key end
+  double *tab;
 
+  // load the batch [pos, pos + 64) of the key (at most to its end; a used-up key is
+  // twisted first) and prepare its draw tables
   __device__ void refill(int lane) {
     uint32_t v;
     if (pos >= MT_N) {
@@ -185,54 +196,154 @@ struct MTWave {
     batch = mt_temper(v);
     bstart = pos;
     bsize = n;
+    prep(lane);
   }
-  // mt19937_next
-  __device__ __forceinline__ uint32_t next(int lane) {
-    if (pos - bstart >= bsize) refill(lane);
-    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)batch, pos - bstart);
-    ++pos;
-    return v;
-  }
-  // legacy_double: (a >> 5, b >> 6), exact in f64
-  __device__ __forceinline__ double rand53(int lane) {
-    const uint32_t a = next(lane) >> 5;
-    const uint32_t b = next(lane) >> 6;
-    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
-  }
-  // legacy_gauss: polar Box-Muller with the cached second deviate
-  __device__ double gauss_next(int lane) {
-    if (has_gauss) {
-      has_gauss = 0;
-      const double t = gauss;
-      gauss = 0.0;
-      return t;
-    }
-    double x1, x2, r2;
-    do {
-      x1 = 2.0 * rand53(lane) - 1.0;
-      x2 = 2.0 * rand53(lane) - 1.0;
-      r2 = x1 * x1 + x2 * x2;
-      r2 = uniform_f64(r2);
-    } while (r2 >= 1.0 || r2 == 0.0);
+  // lane-parallel draw tables of the batch: lane l evaluates rand() at word l and the
+  // polar attempt at word l with the operations of numpy's legacy_double /
+  // legacy_gauss (x = 2 rand() - 1, r2 = x1*x1 + x2*x2, f = sqrt(-2 log(r2) / r2))
+  __device__ void prep(int lane) {
+    const uint32_t w1 = lane_from(batch, lane + 1);
+    const double u = ((double)(batch >> 5) * 67108864.0 + (double)(w1 >> 6)) / 9007199254740992.0;
+    const long long ub = __double_as_longlong(u);
+    const uint32_t lo = lane_from((uint32_t)(ub & 0xffffffffll), lane + 2);
+    const uint32_t hi = lane_from((uint32_t)(ub >> 32), lane + 2);
+    const double u2 = __longlong_as_double((long long)lo | ((long long)hi << 32));
+    const double x1 = 2.0 * u - 1.0;
+    const double x2 = 2.0 * u2 - 1.0;
+    const double r2 = x1 * x1 + x2 * x2;
     const double f = sqrt(-2.0 * log(r2) / r2);
-    gauss = f * x1;
-    has_gauss = 1;
-    return f * x2;
+    tab[lane] = u;
+    tab[64 + lane] = ((r2 < 1.0) & (r2 != 0.0)) ? f : -1.0;   // bitwise &: no branches
+    wave_sync();
   }
-  // randint(0, np): buffered_bounded_masked_uint32 with mask = next pow2 - 1
-  template <int NP> __device__ __forceinline__ int randint(int lane) {
+
+  // The draws of Gibbs iterations in stream order, stages s0..s1:
+  //   0  randint(0, NP)  apf_step2.py:302  buffered_bounded_masked_uint32 -> r
+  //   1  gauss()         :307 (proposal)  legacy_gauss with the cached deviate -> g
+  //   2  rand()          :144 (accept)    legacy_double -> tab[dice_idx]
+  // One loop with ONE refill site, so the table preparation (log, sqrt, division) is
+  // emitted once.  A draw whose words are in the batch is a table read; a batch with
+  // fewer words left than the next draw needs is reloaded from pos, except at the key
+  // end (pos + need > 624), where the draw is assembled word by word across the twist.
+  template <int NP>
+  __device__ void draw(int lane, int s0, int s1, int &r, double &g, int &dice_idx) {
     constexpr uint32_t rng = NP - 1;
     constexpr uint32_t m1 = rng | (rng >> 1);
     constexpr uint32_t m2 = m1 | (m1 >> 2);
     constexpr uint32_t m3 = m2 | (m2 >> 4);
     constexpr uint32_t mask = m3 | (m3 >> 8) | (m3 >> 16);
-    uint32_t v;
-    do {
-      v = next(lane) & mask;
-    } while (v > rng);
-    return (int)v;
+    if (s0 == 0 && s1 == 2) {
+      // the common case first, without the loop: the whole iteration (randint word,
+      // [attempt,] rand pair) lies in the batch and the first attempt is accepted
+      const int p = pos - bstart;
+      if (p + (has_gauss ? 3 : 7) <= bsize) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)batch, p) & mask;
+        if (v <= rng) {
+          r = (int)v;
+          if (has_gauss) {
+            has_gauss = 0;
+            g = gauss;
+            gauss = 0.0;
+            dice_idx = p + 1;
+            pos += 3;
+            return;
+          }
+          const double f = uniform_f64(tab[64 + p + 1]);
+          pos += 5;
+          if (f >= 0.0) {
+            const double x1 = 2.0 * tab[p + 1] - 1.0;
+            const double x2 = 2.0 * tab[p + 3] - 1.0;
+            gauss = uniform_f64(f * x1);
+            has_gauss = 1;
+            g = uniform_f64(f * x2);
+            dice_idx = p + 5;
+            pos += 2;
+            return;
+          }
+          s0 = 1;                     // first attempt rejected: go on with the loop
+        }
+      }
+    }
+    int stage = s0;
+    bool slow = false;
+    int got = 0;
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;   // words gathered across the key end
+    for (;;) {
+      if (stage == 1 && has_gauss) {
+        has_gauss = 0;
+        g = gauss;
+        gauss = 0.0;
+        if (stage == s1) return;
+        stage = 2;
+        continue;
+      }
+      const int need = slow ? 1 : (stage == 0 ? 1 : stage == 1 ? 4 : 2);
+      int p = pos - bstart;
+      if (p + need > bsize) {
+        if (!slow && pos < MT_N && pos + need > MT_N) {
+          slow = true;
+          continue;
+        }
+        refill(lane);
+        p = 0;
+      }
+      if (!slow) {
+        if (stage == 0) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)batch, p) & mask;
+          ++pos;
+          if (v > rng) continue;              // (NP = 19: masked rejection)
+          r = (int)v;
+        } else if (stage == 1) {
+          pos += 4;
+          const double f = uniform_f64(tab[64 + p]);
+          if (f < 0.0) continue;               // rejected attempt
+          const double x1 = 2.0 * tab[p] - 1.0;
+          const double x2 = 2.0 * tab[p + 2] - 1.0;
+          gauss = uniform_f64(f * x1);
+          has_gauss = 1;
+          g = uniform_f64(f * x2);
+        } else {
+          pos += 2;
+          dice_idx = p;
+        }
+      } else {
+        w0 = w1;
+        w1 = w2;
+        w2 = w3;
+        w3 = (uint32_t)__builtin_amdgcn_readlane((int)batch, p);
+        ++pos;
+        if (++got < (stage == 1 ? 4 : 2)) continue;
+        slow = false;
+        got = 0;
+        if (stage == 1) {
+          const double x1 = 2.0 * (((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) / 9007199254740992.0) - 1.0;
+          const double x2 = 2.0 * (((double)(w2 >> 5) * 67108864.0 + (double)(w3 >> 6)) / 9007199254740992.0) - 1.0;
+          const double r2 = uniform_f64(x1 * x1 + x2 * x2);
+          if (!(r2 < 1.0 && r2 != 0.0)) continue;
+          const double f = sqrt(-2.0 * log(r2) / r2);
+          gauss = uniform_f64(f * x1);
+          has_gauss = 1;
+          g = uniform_f64(f * x2);
+        } else {
+          if (lane == 0) tab[128] = ((double)(w2 >> 5) * 67108864.0 + (double)(w3 >> 6)) / 9007199254740992.0;
+          wave_sync();
+          dice_idx = 128;
+        }
+      }
+      if (stage == s1) return;
+      ++stage;
+    }
+  }
+
+  // mt19937_next (raw stream test hook; the sampler draws through draw())
+  __device__ uint32_t next(int lane) {
+    if (pos - bstart >= bsize) refill(lane);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)batch, pos - bstart);
+    ++pos;
+    return v;
   }
 };
+constexpr int kDrawTab = 129;   // doubles of MTWave::tab
 
 // np.random.seed(s): init_genrand (mt19937_seed)
 __device__ inline void mt_seed_serial(uint32_t *key, uint32_t s) {
