@@ -275,3 +275,54 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     assert m[0] == flat.shape[0]
     np.testing.assert_allclose(m[1:1 + s.ps], flat.sum(axis=0), rtol=1e-12)
     np.testing.assert_allclose(m[1 + s.ps:], (flat ** 2).sum(axis=0), rtol=1e-12)
+
+
+@pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
+def test_rng_streams_misaligned(golden, lib_loaded, skip):
+    """Draws that straddle a batch end or the key end (the draw tables' slow paths,
+    DESIGN.md §3): after `skip` raw words the polar attempts (4 words) and rand()
+    pairs (2 words) no longer align with the 624-word key, so some are assembled
+    across the twist.  Same deviates as RandomState, and the same draw count (the raw
+    tail is bit-exact)."""
+    s = make_sampler(golden("c32"))
+    seeds = np.array([4, 77, 2 ** 31 + 9], np.uint32)
+    for kind in ("gauss", "rand"):
+        s.seed(seeds)
+        s.rng_stream("raw", skip)
+        got = s.rng_stream(kind, 900)
+        tail = s.rng_stream("raw", 3)
+        for w, sd in enumerate(seeds):
+            r = np.random.RandomState(int(sd))
+            r.randint(0, 2 ** 32, size=skip, dtype=np.uint64)
+            ref = r.standard_normal(900) if kind == "gauss" else r.random_sample(900)
+            if kind == "gauss":
+                np.testing.assert_allclose(got[w], ref, rtol=3.2e-15, atol=1e-300)
+            else:
+                assert np.array_equal(got[w], ref)
+            assert np.array_equal(tail[w], r.randint(0, 2 ** 32, size=3, dtype=np.uint64))
+
+
+def test_bench_size_walkers_match_oracle(lib_loaded):
+    """BASELINE configs[2] at full size (65,536 walkers, 64x64 two-source synthetic
+    cutout, FAST evaluation, the bench's seeds and start): a walker's chain does not
+    depend on the ensemble around it, so sampled walkers equal the oracle run of their
+    seeds; all chains stay finite."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    n, W, n_it = 64, 65536, 40
+    img, _ = synth.make_image(n, 2, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = initial_parameters(img, synth.guess_values(n, 2), 2)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+    p0[-1] = s.chi_squared(p0)
+    seeds = 1000 + np.arange(W)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (W, 1)))
+    chain = s.run(n_it, burn_in=0, record_stride=4)
+    assert chain.shape == (W, n_it // 4, s.ps) and np.all(np.isfinite(chain))
+    for w in (0, 1, 4097, 31337, W - 1):
+        ref, _ = ora.Walker(dm, err, p0, int(seeds[w])).run(n_it, record_stride=4)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
+    st, tries, acc = s.get_state()
+    assert np.all(tries.sum(axis=1) == n_it) and np.all(acc <= tries)
