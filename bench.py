@@ -213,6 +213,14 @@ def main():
     steps_per_launch = wpg * args.iters
     traffic = load_traffic(args.traffic)
 
+    def traffic_of(mode):
+        # PMC bytes per launch, measured for this config at the default launch shape
+        # (walkers, iterations, stride); null for any other workload
+        if args.walkers or args.iters != 100 or args.stride != 10:
+            return None
+        key = mode if args.config == 2 else f"c{args.config}_{mode}"
+        return (traffic or {}).get(key, {}).get("bytes_per_launch")
+
     def roofline(mode, kernel_ms):
         # achieved = SURVEY.md §8(d)'s algorithmic work per walker-step (the exp-form
         # count, E = 20) x walker-steps per launch / HIP-event kernel time.  The FAST
@@ -231,7 +239,7 @@ def main():
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": achieved / peak,
-            "traffic": (traffic or {}).get(mode, {}).get("bytes_per_launch"),
+            "traffic": traffic_of(mode),
             "kernel": "olpe_gibbs_kernel",
             "kernel_ms": kernel_ms,
             "algorithmic_work_per_walker_step": algo,

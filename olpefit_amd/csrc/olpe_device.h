@@ -789,6 +789,54 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
+// FAST3 guard, per column (when fast3_ok's whole-grid bound fails, e.g. a source far
+// from the grid centre of a 128-pixel cutout, where Q over the whole grid exceeds the
+// range the anchored a_0 can represent).  Per Gaussian: c S^2 km^2 < 600 as in
+// fast3_ok (no a_k overflow, no H underflow) and, in every column j (lane-parallel,
+// the quantities col_term evaluates):
+//   |log rho| < 170                      (rho^4 of the four-row update finite), and
+//   log(a_0 / A) > -700                  (a_0 normal: a_k = a_0 rho^k exact), or
+//   (a - b^2 / 4c) dx^2 >= 100           (Q >= 100 on the whole column: the Gaussian is
+//                                         below A e^-100 there, so an a_0 that underflows
+//                                         only drops values below that).
+// |A| < 1e20 keeps A e^-100 negligible beside any model value.
+template <int NSRC>
+__device__ __forceinline__ bool fast3_ok_cols(const ModelDesc<NSRC> &m, int n, int rows, int kc,
+                                              int lane) {
+  const ColWalk cw(n, lane);
+  const double S = (double)cw.S;
+  const double kcd = (double)kc;
+  const double km = (double)(kc > rows - 1 - kc ? kc : rows - 1 - kc) + 1.0;
+  const double yr = (double)cw.grp;
+  int ok = 1;
+  // not unrolled: the descriptor is in LDS, and the guard must not raise the sampler's
+  // register pressure (an unrolled form spilled)
+#pragma unroll 1
+  for (int g = 0; g < 2 * NSRC; ++g) {
+    const Gauss &q = m.g[g];
+    const double cs = q.k.c * (S * S);
+    const double K = cs * (kcd * (kcd + 1.0));
+    const double amin = q.k.a - (q.k.b * q.k.b) / (4.0 * q.k.c);
+    const double yd = yr - q.y0;
+    ok &= (int)(cs * km * km < 600.0) & (int)(q.k.a >= 0.0) & (int)(q.k.c > 0.0) &
+          (int)(fabs(q.amp) < 1e20) & (int)isfinite(amin);
+#pragma unroll 1
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int j = c0 + cw.jl;
+      const bool act = cw.lane_ok && j < n;
+      const double xd = (double)j - q.x0;
+      const double bx = q.k.b * xd;
+      const double q0 = (q.k.a * (xd * xd) + bx * yd) + q.k.c * (yd * yd);
+      const double d0 = bx * S + (q.k.c * S) * (2.0 * yd + S);
+      const double xe = K - q0;
+      const double xr = d0 + 2.0 * cs * kcd;
+      const int okc = (int)(fabs(xr) < 170.0) & ((int)(xe > -700.0) | (int)(amin * (xd * xd) >= 100.0));
+      ok &= okc | (int)!act;
+    }
+  }
+  return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
 // FAST3's shape tables, tab[2k] = H_wide(k), tab[2k+1] = H_narrow(k), k lane-parallel.
 // `which` selects the sets recomputed (bit 0 wide, bit 1 narrow); the others are copied
 // from `from` (the table of the current state: a Gibbs step changes at most one set).
@@ -1087,7 +1135,16 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
 #ifdef OLPE_DIAG_NO_GUARD
     const bool ok3 = true;                       // diagnostic: guard skipped
 #else
-    const bool ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+    bool ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+    // the per-column guard only where the whole-grid one can fail on a well-placed
+    // model (cutouts wider than 64 columns); at n <= 64 it would cost the sampler
+    // registers for a branch the bench never takes
+    if constexpr (NT == 0 || NT > 64) {
+      if (!ok3) {
+        asm volatile("" ::: "memory");
+        ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane);
+      }
+    }
 #endif
     asm volatile("" ::: "memory");
     if (ok3) {

@@ -326,3 +326,38 @@ def test_bench_size_walkers_match_oracle(lib_loaded):
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
     st, tries, acc = s.get_state()
     assert np.all(tries.sum(axis=1) == n_it) and np.all(acc <= tries)
+
+
+def test_bench_3source_128_matches_oracle(lib_loaded):
+    """BASELINE configs[4]'s workload (3-source 128x128 synthetic cutout, FAST, the
+    bench's seeds and start): the third source sits 32 px off-centre, so the whole-grid
+    FAST3 guard fails and the per-column guard (fast3_ok_cols) admits FAST3; model and
+    chi^2 at the start vector at the FAST tolerance against EXACT, and 3 walkers x 300
+    iterations against the oracle run of their seeds."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    n, nsrc, n_it = 128, 3, 300
+    img, _ = synth.make_image(n, nsrc, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    with np.errstate(all="ignore"):
+        ref_model = ora.build_analytical_model(p0, n, nsrc)
+        p0[-1] = float(ora.chi_squared(dm, ref_model, err))
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    m = s.build_analytical_model(p0)
+    assert np.max(np.abs(m - ref_model)) <= TOL["fast"]["model"] * np.max(np.abs(ref_model))
+    assert abs(s.chi_squared(p0) - p0[-1]) <= TOL["fast"]["chi"] * p0[-1]
+    W = 4096
+    seeds = 1000 + np.arange(W)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (W, 1)))
+    s.enable_trace(True)
+    chain = s.run(n_it, burn_in=0, record_stride=3)
+    tr = s.trace(n_it)
+    assert np.all(np.isfinite(chain))
+    for w in (0, 1777, W - 1):
+        ref, rtr = ora.Walker(dm, err, p0, int(seeds[w]), nsrc=nsrc).run(n_it, record_stride=3,
+                                                                         trace=True)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
+        assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
