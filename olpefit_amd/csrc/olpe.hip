@@ -121,10 +121,14 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
   s[0] = k.a; s[1] = k.b; s[2] = k.c;
 }
 
+#ifndef OLPE_GLOBAL_WAVES_PER_EU
+#define OLPE_GLOBAL_WAVES_PER_EU 3
+#endif
 template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // The global-memory (large cutout) variant runs 4-wave workgroups and waits on L2: it
-// is asked to fit 4 of them per CU (128 VGPRs; 2 waves per SIMD otherwise): +7 %
-__global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : 4) void olpe_gibbs_kernel(GibbsArgs A) {
+// is asked to fit 3 of them per CU (168 VGPRs, no spills; 3-source 128x128 +0.9 % over
+// 4 per CU at 128 VGPRs, +4.5 % over 2 per CU)
+__global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
   constexpr int NP = L::NP, PS = L::PS;
