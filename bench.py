@@ -145,6 +145,9 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on device 0, no RCCL "
+                         "all-gather (RCCL refuses two ranks on one device)")
     args = ap.parse_args()
 
     from olpefit_amd import dist as odist
@@ -159,7 +162,7 @@ def main():
     if args.walkers:
         wpg = args.walkers
     img, _ = synth.make_image(n, nsrc, 0)
-    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=local)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=0 if args.share_gpu else local)
     # step-1 style start (apf_step2.py:264-289) for every walker
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
@@ -194,7 +197,7 @@ def main():
 
     # end-of-run exchange: RCCL all-gather of final walker states
     gather_ms = None
-    if world > 1:
+    if world > 1 and not args.share_gpu:
         uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
         s.comm_init(uid, world, rank)
         barrier()
