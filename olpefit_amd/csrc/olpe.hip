@@ -10,6 +10,7 @@
 //   olpe_stream_kernel RNG stream dump (test hook)
 #include <hip/hip_runtime.h>
 
+#include <limits.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -64,6 +65,10 @@ struct GibbsArgs {
   double *chain;       // [W][nrows][PS]
   long long accept_min;
   double *trace;       // [W][n_iters][6] or null
+  // walker queue: null = one walker per wave at blockIdx*WPB + wave; otherwise each
+  // wave takes walkers qbase.. from the counter until it passes W (persistent grid)
+  unsigned long long *queue;
+  unsigned long long qbase;
 };
 
 constexpr int kTraceF = 6;
@@ -161,242 +166,269 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
   __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
 
-  const long long w = (long long)blockIdx.x * WPB + wave;
-  if (w >= A.W) return;
+  // Arguments used once per walker are read where they are used, through a kernarg
+  // pointer the compiler cannot see through, so that they do not hold SGPRs across
+  // the sampler loop (SGPR pressure spills into VGPR lanes).
+  auto K = []() {
+    const __attribute__((address_space(4))) GibbsArgs *p =
+        (const __attribute__((address_space(4))) GibbsArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+  };
 
-  // ---- walker state -> LDS slice
-  if (lane < NP) {
-    s_tries[lane] = A.tries[w * NP + lane];
-    s_acc[lane] = A.accepts[w * NP + lane];
-  }
-  if (lane < PS) st[lane] = A.state[w * PS + lane];
-  wave_sync();
-  if (lane == 0) {
-    const Trig t1 = make_trig<FAST>(st[L::T1]), t2 = make_trig<FAST>(st[L::T2]);
-    st_trig(st + WS::OT1, t1);
-    st_trig(st + WS::OT2, t2);
-    st_coef(st + WS::OC1, make_coef<FAST>(st[L::S1X], st[L::S1Y], t1));
-    st_coef(st + WS::OC2, make_coef<FAST>(st[L::S2X], st[L::S2Y], t2));
-  }
-  wave_sync();
-
-  MTWave mt;
-  mt.key = A.mt + (size_t)w * MT_N;
-  mt.pos = __builtin_amdgcn_readfirstlane(A.mt_pos[w]);
-  mt.bstart = mt.pos;
-  mt.bsize = 0;
-  mt.batch = 0;
-  mt.has_gauss = __builtin_amdgcn_readfirstlane(A.has_gauss[w]);
-  mt.gauss = uniform_f64(A.gauss[w]);
-  mt.tab = drawtab;
-
-  int ndone = 0;
-  long long done_at = A.done_at[w];
-  if (A.accept_min > 0) {
-    for (int k = 0; k < NP; ++k) ndone += (s_tries[k] >= (uint32_t)A.accept_min);
-    ndone = __builtin_amdgcn_readfirstlane(ndone);
-  }
-
+  // walker of this wave: static, or the next one off the queue -- a wave that
+  // finishes its walker takes another at once, instead of idling until the slowest
+  // wave of its workgroup is done (waves of one SIMD run at different speeds: VALU
+  // issue goes by age)
+  // (the host keeps W < 2^31, so the walker index is a 32-bit value)
+  auto take = [&]() -> int {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(K()->queue, 1ull) - K()->qbase;
+    const unsigned d = v > 0x7fffffffull ? 0x7fffffffu : (unsigned)v;
+    return __builtin_amdgcn_readfirstlane((int)d);
+  };
   // chain rows: the iteration (0-based, this launch) of the next record -- count =
   // count0 + it + 1 >= burn_in and (count - burn_in) % stride == 0 -- and its row,
-  // advanced by 32-bit addition (host: n_iters < 2^31)
+  // advanced by 32-bit addition (host: n_iters < 2^31); the same for every walker
   const int niter = (int)A.n_iters;
   const int rstride = (int)A.stride;
   const int nrows = (int)A.nrows;
-  int rec_it = -1, rec_row = 0;
+  int rec_it0 = -1, rec_row0 = 0;
   if (A.stride > 0) {
     const long long c1 = A.count0 + 1;
     const long long k = c1 > A.burn_in ? (c1 - A.burn_in + A.stride - 1) / A.stride : 0;
     const long long first = A.burn_in + k * A.stride - c1;
-    rec_it = first < niter ? (int)first : -1;
-    rec_row = (int)(k - A.row0);
+    rec_it0 = first < niter ? (int)first : -1;
+    rec_row0 = (int)(k - A.row0);
   }
-  double *chain_w = A.chain + (size_t)w * A.nrows * PS;
-
-  HCache hcache;
-  ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
-  ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
-  __builtin_amdgcn_s_setprio(1);
-#ifdef OLPE_DIAG_TIMING
-  unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long dt_last = __builtin_amdgcn_s_memtime();
-#endif
-  for (int it = 0; it < niter; ++it) {
-    // the iteration's draws: randint(0, NP) (apf_step2.py:302), the proposal's gauss()
-    // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
-    int r0 = 0, dice_idx = 0;
-    double g = 0.0;
-#ifdef OLPE_DIAG_NO_GAUSS
-    mt.template draw<NP>(lane, 0, 0, r0, g, dice_idx);
-    mt.template draw<NP>(lane, 2, 2, r0, g, dice_idx);
-    g = 0.01 * (double)(r0 - 8);                  // diagnostic: no polar draw
-#else
-    mt.template draw<NP>(lane, 0, 2, r0, g, dice_idx);
-#endif
-    const int r = __builtin_amdgcn_readfirstlane(r0);
-    // total_tries[rand] += 1  (:304)
-    const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
+  int w = A.queue ? take() : (int)blockIdx.x * WPB + wave;
+  for (; w < K()->W; w = K()->queue ? take() : INT_MAX) {
+    // ---- walker state -> LDS slice
+    if (lane < NP) {
+      s_tries[lane] = K()->tries[(size_t)w * NP + lane];
+      s_acc[lane] = K()->accepts[(size_t)w * NP + lane];
+    }
+    if (lane < PS) st[lane] = K()->state[(size_t)w * PS + lane];
     wave_sync();
-    if (lane == 0) s_tries[r] = tr;
-    if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) ++ndone;
-    DT_MARK(0);
-
-    // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
-    const double cur = uniform_f64(st[r]);
-    const double wr = width_of<NSRC>(r);
-    double nv;
-    if ((L::LOGMASK >> r) & 1u) {
-      if constexpr (FAST) {
-        // 10**(log10(cur) + w g) = cur * e^(w g ln10): no log10, and the exponent is
-        // small (|w g ln10| < 0.06 for |g| < 10) -- a degree-9 Taylor polynomial, the
-        // table exp beyond; cur < 0 keeps the reference's NaN (log10 of a negative)
-        const double x = (wr * g) * 2.302585092994046;
-        double e;
-        if (fabs(x) < 0.0625) {
-          double p = fma(x, 1.0 / 362880, 1.0 / 40320);
-          p = fma(x, p, 1.0 / 5040);
-          p = fma(x, p, 1.0 / 720);
-          p = fma(x, p, 1.0 / 120);
-          p = fma(x, p, 1.0 / 24);
-          p = fma(x, p, 1.0 / 6);
-          p = fma(x, p, 0.5);
-          p = fma(x, p, 1.0);
-          e = fma(x, p, 1.0);
-        } else {
-          e = ExpTab{etab}(x);
-        }
-        nv = cur < 0.0 ? __builtin_nan("") : cur * e;
-      } else {
-        const double lv = log10(cur);
-        nv = exp10(lv + wr * g);   // 10**lognew (apf_step2.py:69)
-      }
-    } else {
-      nv = cur + wr * g;
-    }
-    nv = uniform_f64(nv);
-    DT_MARK(1);
-
-    // coefficient sets of the proposal: only the set that r touches is rebuilt
-    auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
-    const int grp = (r == L::S1X || r == L::S1Y || r == L::T1) ? 1
-                  : (r == L::S2X || r == L::S2Y || r == L::T2) ? 2 : 0;
-    Coef C1p, C2p;
-    if (grp == 1) {
-      const Trig t = (r == L::T1) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT1);
-      C1p = make_coef<FAST>(q(L::S1X), q(L::S1Y), t);
-      if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
-    } else {
-      C1p = ld_coef(st + WS::OC1);
-    }
-    if (grp == 2) {
-      const Trig t = (r == L::T2) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT2);
-      C2p = make_coef<FAST>(q(L::S2X), q(L::S2Y), t);
-      if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
-    } else {
-      C2p = ld_coef(st + WS::OC2);
-    }
-    // the step's model descriptor goes to LDS (the sweep loads each field where it is
-    // used instead of holding 6*G doubles in registers across it), built lane-parallel:
-    // lane g < G writes Gaussian g with make_model's operations, lane G the background
-    if (lane < 2 * NSRC) {
-      const int s = lane >> 1;
-      const bool narrow = lane & 1;
-      auto ql = [&](int k) -> double { return (k == r) ? nv : st[k]; };
-      const double tot = ql(L::sa(s)) - ql(L::OFF);
-      const double wide = tot * ql(L::RATIO);
-      const double xc = ql(L::sx(s)), yc = ql(L::sy(s));
-      // component-wise selects (a select of whole structs goes through scratch)
-      const Coef C{narrow ? C1p.a : C2p.a, narrow ? C1p.b : C2p.b, narrow ? C1p.c : C2p.c};
-      const double dx = narrow ? 0.0 : ql(L::DX), dy = narrow ? 0.0 : ql(L::DY);
-      mdl->g[lane] = Gauss{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
-                           narrow ? yc : yc + dy, C};
-    } else if (lane == 2 * NSRC) {
-      mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
+    if (lane == 0) {
+      const Trig t1 = make_trig<FAST>(st[L::T1]), t2 = make_trig<FAST>(st[L::T2]);
+      st_trig(st + WS::OT1, t1);
+      st_trig(st + WS::OT2, t2);
+      st_coef(st + WS::OC1, make_coef<FAST>(st[L::S1X], st[L::S1Y], t1));
+      st_coef(st + WS::OC2, make_coef<FAST>(st[L::S2X], st[L::S2Y], t2));
     }
     wave_sync();
-    DT_MARK(2);
 
-    // build_analytical_model + chi_squared (:314-316)
-    // the step's scalar control is a latency-bound chain: it runs at raised wave
-    // priority so that it is not queued behind the other waves' sweeps
-    __builtin_amdgcn_s_setprio(0);
-    hcache.grp = grp;
-    const unsigned gmask = gauss_mask<NSRC>(r);
-    const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab,
-                                                     &hcache, &ccache, gmask);
+    MTWave mt;
+    mt.key = K()->mt + (size_t)w * MT_N;
+    mt.pos = __builtin_amdgcn_readfirstlane(K()->mt_pos[w]);
+    mt.bstart = mt.pos;
+    mt.bsize = 0;
+    mt.batch = 0;
+    mt.has_gauss = __builtin_amdgcn_readfirstlane(K()->has_gauss[w]);
+    mt.gauss = uniform_f64(K()->gauss[w]);
+    mt.tab = drawtab;
+
+    int ndone = 0;
+    long long done_at = K()->done_at[w];
+    if (A.accept_min > 0) {
+      for (int k = 0; k < NP; ++k) ndone += (s_tries[k] >= (uint32_t)A.accept_min);
+      ndone = __builtin_amdgcn_readfirstlane(ndone);
+    }
+
+    int rec_it = rec_it0, rec_row = rec_row0;
+    double *chain_w = K()->chain + (size_t)w * nrows * PS;
+
+    HCache hcache;
+    ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
+    ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
+#pragma unroll
+    for (int g = 0; g < 2 * NSRC; ++g) ccache.E[g] = ccache.R[g] = 0.0;
     __builtin_amdgcn_s_setprio(1);
-    DT_MARK(3);
-    const double chi = wave_sum(part);
-    DT_MARK(4);
-
-    // accept_reject (:139-148)
-    // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
-    const double la = -(chi - st[PS - 1]) / 2.;
-    const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
-    const double dice = drawtab[dice_idx];
-    const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
-    hcache.after(acc);
-    if constexpr (FAST && NT != 0 && NT <= 64) {
-#ifndef OLPE_DIAG_NO_REFRESH
-      if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
+#ifdef OLPE_DIAG_TIMING
+    unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long dt_last = __builtin_amdgcn_s_memtime();
 #endif
-      ccache.pend = 0;              // parked terms belong to this step only
-    }
-    wave_sync();
-    if (acc && lane == 0) {
-      s_acc[r] = s_acc[r] + 1u;
-      st[r] = nv;
-      st[PS - 1] = chi;
-      if (grp) {
-        double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
-        double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
-        for (int k = 0; k < 3; ++k) dt[k] = st[WS::OPT + k];
-        for (int k = 0; k < 3; ++k) dc[k] = st[WS::OPC + k];
+    for (int it = 0; it < niter; ++it) {
+      // the iteration's draws: randint(0, NP) (apf_step2.py:302), the proposal's gauss()
+      // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
+      int r0 = 0, dice_idx = 0;
+      double g = 0.0;
+#ifdef OLPE_DIAG_NO_GAUSS
+      mt.template draw<NP>(lane, 0, 0, r0, g, dice_idx);
+      mt.template draw<NP>(lane, 2, 2, r0, g, dice_idx);
+      g = 0.01 * (double)(r0 - 8);                  // diagnostic: no polar draw
+#else
+      mt.template draw<NP>(lane, 0, 2, r0, g, dice_idx);
+#endif
+      const int r = __builtin_amdgcn_readfirstlane(r0);
+      // total_tries[rand] += 1  (:304)
+      const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
+      wave_sync();
+      if (lane == 0) s_tries[r] = tr;
+      if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) ++ndone;
+      DT_MARK(0);
+
+      // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
+      const double cur = uniform_f64(st[r]);
+      const double wr = width_of<NSRC>(r);
+      double nv;
+      if ((L::LOGMASK >> r) & 1u) {
+        if constexpr (FAST) {
+          // 10**(log10(cur) + w g) = cur * e^(w g ln10): no log10, and the exponent is
+          // small (|w g ln10| < 0.06 for |g| < 10) -- a degree-9 Taylor polynomial, the
+          // table exp beyond; cur < 0 keeps the reference's NaN (log10 of a negative)
+          const double x = (wr * g) * 2.302585092994046;
+          double e;
+          if (fabs(x) < 0.0625) {
+            double p = fma(x, 1.0 / 362880, 1.0 / 40320);
+            p = fma(x, p, 1.0 / 5040);
+            p = fma(x, p, 1.0 / 720);
+            p = fma(x, p, 1.0 / 120);
+            p = fma(x, p, 1.0 / 24);
+            p = fma(x, p, 1.0 / 6);
+            p = fma(x, p, 0.5);
+            p = fma(x, p, 1.0);
+            e = fma(x, p, 1.0);
+          } else {
+            e = ExpTab{etab}(x);
+          }
+          nv = cur < 0.0 ? __builtin_nan("") : cur * e;
+        } else {
+          const double lv = log10(cur);
+          nv = exp10(lv + wr * g);   // 10**lognew (apf_step2.py:69)
+        }
+      } else {
+        nv = cur + wr * g;
       }
-    }
-    wave_sync();
-    if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
-    DT_MARK(5);
+      nv = uniform_f64(nv);
+      DT_MARK(1);
+
+      // coefficient sets of the proposal: only the set that r touches is rebuilt
+      auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
+      const int grp = (r == L::S1X || r == L::S1Y || r == L::T1) ? 1
+                    : (r == L::S2X || r == L::S2Y || r == L::T2) ? 2 : 0;
+      Coef C1p, C2p;
+      if (grp == 1) {
+        const Trig t = (r == L::T1) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT1);
+        C1p = make_coef<FAST>(q(L::S1X), q(L::S1Y), t);
+        if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
+      } else {
+        C1p = ld_coef(st + WS::OC1);
+      }
+      if (grp == 2) {
+        const Trig t = (r == L::T2) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT2);
+        C2p = make_coef<FAST>(q(L::S2X), q(L::S2Y), t);
+        if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
+      } else {
+        C2p = ld_coef(st + WS::OC2);
+      }
+      // the step's model descriptor goes to LDS (the sweep loads each field where it is
+      // used instead of holding 6*G doubles in registers across it), built lane-parallel:
+      // lane g < G writes Gaussian g with make_model's operations, lane G the background
+      if (lane < 2 * NSRC) {
+        const int s = lane >> 1;
+        const bool narrow = lane & 1;
+        auto ql = [&](int k) -> double { return (k == r) ? nv : st[k]; };
+        const double tot = ql(L::sa(s)) - ql(L::OFF);
+        const double wide = tot * ql(L::RATIO);
+        const double xc = ql(L::sx(s)), yc = ql(L::sy(s));
+        // component-wise selects (a select of whole structs goes through scratch)
+        const Coef C{narrow ? C1p.a : C2p.a, narrow ? C1p.b : C2p.b, narrow ? C1p.c : C2p.c};
+        const double dx = narrow ? 0.0 : ql(L::DX), dy = narrow ? 0.0 : ql(L::DY);
+        mdl->g[lane] = Gauss{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
+                             narrow ? yc : yc + dy, C};
+      } else if (lane == 2 * NSRC) {
+        mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
+      }
+      wave_sync();
+      DT_MARK(2);
+
+      // build_analytical_model + chi_squared (:314-316)
+      // the step's scalar control is a latency-bound chain: it runs at raised wave
+      // priority so that it is not queued behind the other waves' sweeps
+      __builtin_amdgcn_s_setprio(0);
+      hcache.grp = grp;
+      const unsigned gmask = gauss_mask<NSRC>(r);
+      const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab,
+                                                       &hcache, &ccache, gmask);
+      __builtin_amdgcn_s_setprio(1);
+      DT_MARK(3);
+      const double chi = wave_sum(part);
+      DT_MARK(4);
+
+      // accept_reject (:139-148)
+      // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
+      const double la = -(chi - st[PS - 1]) / 2.;
+      const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
+      const double dice = drawtab[dice_idx];
+      const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
+      hcache.after(acc);
+      if constexpr (FAST && NT != 0 && NT <= 64) {
+#ifndef OLPE_DIAG_NO_REFRESH
+        if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
+#endif
+        ccache.pend = 0;              // parked terms belong to this step only
+      }
+      wave_sync();
+      if (acc && lane == 0) {
+        s_acc[r] = s_acc[r] + 1u;
+        st[r] = nv;
+        st[PS - 1] = chi;
+        if (grp) {
+          double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
+          double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
+          for (int k = 0; k < 3; ++k) dt[k] = st[WS::OPT + k];
+          for (int k = 0; k < 3; ++k) dc[k] = st[WS::OPC + k];
+        }
+      }
+      wave_sync();
+      if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
+      DT_MARK(5);
 
 #ifndef OLPE_DIAG_TIMING
-    if (A.trace && lane == 0) {
-      double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
-      t[0] = (double)r;
-      t[1] = nv;
-      t[2] = chi;
-      t[3] = dice;
-      t[4] = p_accept;
-      t[5] = acc ? 1.0 : 0.0;
-    }
+      if (A.trace && lane == 0) {
+        double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
+        t[0] = (double)r;
+        t[1] = nv;
+        t[2] = chi;
+        t[3] = dice;
+        t[4] = p_accept;
+        t[5] = acc ? 1.0 : 0.0;
+      }
 #endif
-    // chain record (:342-351, generalised to a stride)
-    if (it == rec_it) {
-      if (rec_row >= 0 && rec_row < nrows && lane < PS) chain_w[rec_row * PS + lane] = st[lane];
-      rec_it += rstride;
-      ++rec_row;
+      // chain record (:342-351, generalised to a stride)
+      if (it == rec_it) {
+        if (rec_row >= 0 && rec_row < nrows && lane < PS) chain_w[rec_row * PS + lane] = st[lane];
+        rec_it += rstride;
+        ++rec_row;
+      }
+      DT_MARK(6);
     }
-    DT_MARK(6);
-  }
 #ifdef OLPE_DIAG_TIMING
-  if (A.trace && lane < 9) {
-    unsigned long long v = lane == 7 ? ccache.n_setup : lane == 8 ? ccache.n_refresh : 0;
-    for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
-    A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
-  }
+    if (A.trace && lane < 9) {
+      unsigned long long v = lane == 7 ? ccache.n_setup : lane == 8 ? ccache.n_refresh : 0;
+      for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
+      A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
+    }
 #endif
 
-  // ---- write back
-  wave_sync();
-  if (lane < PS) A.state[w * PS + lane] = st[lane];
-  if (lane < NP) {
-    A.tries[w * NP + lane] = s_tries[lane];
-    A.accepts[w * NP + lane] = s_acc[lane];
-  }
-  if (lane == 0) {
-    A.mt_pos[w] = mt.pos;
-    A.has_gauss[w] = mt.has_gauss;
-    A.gauss[w] = mt.gauss;
-    A.done_at[w] = done_at;
+    // ---- write back (the walker index laundered: its per-lane addresses are
+    // recomputed here, not kept live across the sampler loop from the loads above)
+    wave_sync();
+    asm volatile("" : "+s"(w));
+    if (lane < PS) K()->state[(size_t)w * PS + lane] = st[lane];
+    if (lane < NP) {
+      K()->tries[(size_t)w * NP + lane] = s_tries[lane];
+      K()->accepts[(size_t)w * NP + lane] = s_acc[lane];
+    }
+    if (lane == 0) {
+      K()->mt_pos[w] = mt.pos;
+      K()->has_gauss[w] = mt.has_gauss;
+      K()->gauss[w] = mt.gauss;
+      K()->done_at[w] = done_at;
+    }
+    wave_sync();      // the slice is reused by the wave's next walker
   }
 }
 
@@ -561,8 +593,22 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
                                160 * 1024));
     attr_set = true;
   }
-  const unsigned blocks = (unsigned)((a.W + WPB - 1) / WPB);
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, a);
+  unsigned blocks = (unsigned)((a.W + WPB - 1) / WPB);
+  GibbsArgs q = a;
+  q.queue = nullptr;
+  q.qbase = 0;
+  if (LDS && c->queue_on && c->d_queue) {
+    // persistent grid: as many workgroups as fit on the device at once, the walkers
+    // handed out by the queue
+    int per_cu = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
+    const unsigned resident = (unsigned)std::max(1, per_cu) * (unsigned)c->n_cu;
+    if (blocks > resident) blocks = resident;
+    q.queue = c->d_queue;
+    q.qbase = c->qbase;
+    c->qbase += (unsigned long long)a.W + (unsigned long long)blocks * WPB;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
   return OLPE_OK;
 }
@@ -685,10 +731,18 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   }
   (void)hipEventCreate(&c->ev0);
   (void)hipEventCreate(&c->ev1);
-  if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix))) {
+  if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
+      (rc = dev_alloc(&c->d_queue, 1))) {
     olpe_destroy(c);
     return rc;
   }
+  if (hipMemset(c->d_queue, 0, sizeof(unsigned long long)) != hipSuccess ||
+      hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
+          hipSuccess || c->n_cu <= 0) {
+    olpe_destroy(c);
+    return set_err(OLPE_EHIP, "walker queue setup failed");
+  }
+  if (const char *e = getenv("OLPE_NO_QUEUE")) c->queue_on = atoi(e) == 0;  // A/B only
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 == hipSuccess)
     e2 = hipMemcpy(c->d_DW, hDW.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
@@ -707,7 +761,7 @@ void olpe_destroy(olpe_ctx *c) {
   olpe_comm_release(c);
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
-                  c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2};
+                  c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -995,21 +995,33 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         acc = act ? fma(t, t, acc) : acc;
       }
     };
-    // four rows per update (the unrolled row loop): row k+r sums a_k rho^r (r = 0..3)
-    // with fmas and a_(k+4) = a_k rho^4 -- 5m-1 operations per set of m Gaussians per
-    // four rows instead of 8m-4, so 8.5 instead of 10 FP64 per pixel for two sources
-    // (+5 %; pairs of rows: 9 per pixel, +4 %).  The powers are formed once per
-    // column; the recurrence rounds 16 times instead of 64 down a 64-row column.
-    double rp[4][G];
+    // RU rows per update (the unrolled row loop): row k+r sums a_k rho^r (r < RU)
+    // with fmas and a_(k+RU) = a_k rho^RU.  Per set of m Gaussians: RU = 2 costs 3m-1
+    // operations per two rows (9 FP64 per pixel for two sources), RU = 4 5m-1 per four
+    // rows (8.5), against 2m-1 per row without it (10).  RU = 2 for the 2-source 64x64
+    // sampler: with the walker queue it spilled less (16 VGPRs fewer for the powers),
+    // 518 vs 502 M walker-steps/s on one box; RU = 4 elsewhere (3-source 128x128: 88.2
+    // vs 85.7 M).  The powers are formed once per column; the recurrence rounds n/RU
+    // times down a column.
+#ifdef OLPE_ROWU
+    constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
+#else
+    constexpr int RU = (NSRC == 2 && NT == 64) ? 2 : 4;
+#endif
+    double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       rp[1][g] = rho[g];
-      rp[2][g] = rho[g] * rho[g];
-      rp[3][g] = rp[2][g] * rho[g];
-      rp[0][g] = rp[2][g] * rp[2][g];
+      if constexpr (RU == 4) {
+        rp[2][g] = rho[g] * rho[g];
+        rp[3][g] = rp[2][g] * rho[g];
+        rp[0][g] = rp[2][g] * rp[2][g];
+      } else {
+        rp[0][g] = rho[g] * rho[g];
+      }
     }
     auto row4 = [&](const double2 *h, const double2 *dw) {
-      double sw[4], sn[4];
+      double sw[RU], sn[RU];
       sw[0] = av[0];
       sn[0] = av[1];
 #pragma unroll
@@ -1018,7 +1030,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         sn[0] = sn[0] + av[2 * s + 1];
       }
 #pragma unroll
-      for (int r = 1; r < 4; ++r) {
+      for (int r = 1; r < RU; ++r) {
         sw[r] = av[2 * NSRC - 2] * rp[r][2 * NSRC - 2];
         sn[r] = av[2 * NSRC - 1] * rp[r][2 * NSRC - 1];
 #pragma unroll
@@ -1030,7 +1042,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 #pragma unroll
       for (int g = 0; g < G; ++g) av[g] = av[g] * rp[0][g];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < RU; ++r) {
         const double mod = fma(sn[r], h[r].y, fma(sw[r], h[r].x, bg));
         const double t = fma(-mod, dw[r].y, dw[r].x);
         acc = act ? fma(t, t, acc) : acc;
@@ -1040,7 +1052,31 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     if (!WRITE && NT != 0 && rows % BLK == 0) {
       const int rstep = cw.S * n;
       const double2 *p = DW + cw.grp * n + jj;
-      double2 cur[BLK], nxt[BLK], hc[BLK], hn[BLK];
+      double2 cur[BLK], nxt[BLK];
+#ifndef OLPE_H_PREFETCH
+      // the shape-table rows (wave-uniform broadcast reads) are read with their block;
+      // only the cutout rows are prefetched a block ahead (16 VGPRs fewer)
+      double2 hc[BLK];
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) cur[k] = p[k * rstep];
+      const int R = NT >= 64 ? NT : rows;
+#pragma unroll 16
+      for (int b0 = 0; b0 < R; b0 += BLK) {
+        const bool more = b0 + BLK < R;
+        const double2 *pn = p + (more ? BLK * rstep : 0);
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) {
+          hc[k] = hr[b0 + k];
+          nxt[k] = pn[k * rstep];
+        }
+#pragma unroll
+        for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+        p = pn;
+      }
+#else
+      double2 hc[BLK], hn[BLK];
 #pragma unroll
       for (int k = 0; k < BLK; ++k) {
         cur[k] = p[k * rstep];
@@ -1060,7 +1096,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           hn[k] = hr[hb + k];
         }
 #pragma unroll
-        for (int k = 0; k < BLK; k += 4) row4(hc + k, cur + k);
+        for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
           cur[k] = nxt[k];
@@ -1068,6 +1104,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         }
         p = pn;
       }
+#endif
     } else {
       int k = 0;
 #pragma unroll 2

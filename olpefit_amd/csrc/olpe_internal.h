@@ -41,6 +41,12 @@ struct olpe_ctx {
   // scratch for olpe_model / olpe_chi2_batch
   double *d_scratch = nullptr, *d_scratch2 = nullptr;
   size_t scratch_cap = 0, scratch2_cap = 0;
+  // walker queue of the sampler (one 64-bit counter; each launch takes W + its waves
+  // from it, so no reset between launches): qbase = the counter's value at launch
+  unsigned long long *d_queue = nullptr;
+  unsigned long long qbase = 0;
+  bool queue_on = true;
+  int n_cu = 0;
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;
