@@ -606,10 +606,12 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
     if (blocks > resident) blocks = resident;
     q.queue = c->d_queue;
     q.qbase = c->qbase;
-    c->qbase += (unsigned long long)a.W + (unsigned long long)blocks * WPB;
   }
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
+  // the launch takes W + (its waves) values off the counter: the next launch's base
+  // (advanced only once the launch is in the stream)
+  if (q.queue) c->qbase += (unsigned long long)a.W + (unsigned long long)blocks * WPB;
   return OLPE_OK;
 }
 

@@ -361,3 +361,29 @@ def test_bench_3source_128_matches_oracle(lib_loaded):
                                                                          trace=True)
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
         assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
+
+
+def test_walker_queue_equals_static_mapping(golden, lib_loaded, monkeypatch):
+    """The persistent sampler hands walkers out from a device counter (DESIGN.md §3);
+    with more walkers than resident waves (4,099 > 256 CUs x 16) some waves run two.
+    Over three launches (the counter is never reset: each launch's base advances by
+    W + its waves) every walker's chain, state, counters and RNG equal the static
+    one-walker-per-wave mapping's bit for bit."""
+    g = golden("c64")
+    W = 4099
+    seeds = 7000 + np.arange(W)
+    out = []
+    for no_queue in ("0", "1"):
+        monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
+        s = make_sampler(g, "fast")
+        s.seed(seeds)
+        s.set_state(np.tile(g["p_init"], (W, 1)))
+        chains = [s.run(n, burn_in=0, record_stride=5) for n in (30, 45, 25)]
+        out.append((chains, s.get_state(), s.rng_state()))
+        s.close()
+    (ca, sa, ra), (cb, sb, rb) = out
+    for x, y in zip(ca, cb):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(sa + ra, sb + rb):
+        np.testing.assert_array_equal(x, y)
+    assert np.all(sa[1].sum(axis=1) == 100)
