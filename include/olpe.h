@@ -22,6 +22,7 @@
 #ifndef OLPE_H
 #define OLPE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -34,6 +35,7 @@ extern "C" {
 #define OLPE_ENOMEM (-3)  /* device allocation failed */
 #define OLPE_ESTATE (-4)  /* call out of order (e.g. run before seeding) */
 #define OLPE_ECOMM (-5)   /* RCCL error */
+#define OLPE_EIO (-6)     /* file write failed */
 
 #define OLPE_DTYPE_F32 0
 #define OLPE_DTYPE_F64 1
@@ -134,6 +136,21 @@ int olpe_trace_read(olpe_ctx *ctx, double *out);
 int olpe_sync(olpe_ctx *ctx);
 /* Duration (ms, HIP events on the launch stream) of the last sampler launch. */
 int olpe_last_kernel_ms(olpe_ctx *ctx, double *ms);
+
+/* --- chain files (apf_step2.py:342-360; 3body/apf_step2_3body.py:381-399) ---------
+ * Host-only (no GPU needed).  Rows are formatted as the reference's csv.writer writes
+ * a list of float rows: repr() of each value (shortest round-trip digits, fixed
+ * notation for decimal exponents -4..15, 'nan'/'inf'), ',' between fields, "\r\n"
+ * after each row.  nan_row != 0 prepends the all-NaN row the reference seeds
+ * total_parameters with (apf_step2.py:278-279). */
+/* Format rows [nrows][ncols] into out (cap bytes; out may be NULL to query the size):
+ * *len_out = bytes of the text. */
+int olpe_csv_format(const double *rows, long long nrows, int ncols, int nan_row, char *out,
+                    size_t cap, size_t *len_out);
+/* Write nfiles chain files: file i gets chains[i][nrows][ncols] (the per-walker
+ * {rank}_finalarray_mpi.csv), from `threads` writer threads (0 = one per core). */
+int olpe_csv_write_chains(const char *const *paths, const double *chains, int nfiles,
+                          long long nrows, int ncols, int nan_row, int threads);
 
 /* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */

@@ -58,6 +58,9 @@ SIGNATURES = {
     "olpe_trace_read": (_i, [_P, _pd]),
     "olpe_sync": (_i, [_P]),
     "olpe_last_kernel_ms": (_i, [_P, _pd]),
+    "olpe_csv_format": (_i, [_pd, _ll, _i, _i, C.c_char_p, C.c_size_t,
+                             C.POINTER(C.c_size_t)]),
+    "olpe_csv_write_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _i, _i, _i]),
     "olpe_comm_unique_id": (_i, [_pu8]),
     "olpe_comm_init": (_i, [_P, _pu8, _i, _i]),
     "olpe_comm_allgather_state": (_i, [_P, _pd]),

@@ -64,17 +64,45 @@ def read_step2a(path: str):
     return np.atleast_2d(a)[-1:][0]
 
 
-def format_rows(chain) -> str:
+def format_rows(chain, nan_row: bool = False) -> str:
     """CSV text ``csv.writer`` produces for ``writerows(rows)`` of float rows: ','
-    separator, '\\r\\n' terminator, shortest-repr floats, NaN as 'nan'."""
-    lines = [",".join([repr(v) for v in row]) for row in np.asarray(chain, dtype=np.float64).tolist()]
-    return "".join(line + "\r\n" for line in lines)
+    separator, '\\r\\n' terminator, repr() floats, NaN as 'nan' (libolpe's native
+    formatter, olpe_csv_format); ``nan_row`` prepends the reference's all-NaN row."""
+    import ctypes as C
+    from . import _lib
+    from ._lib import check
+    rows = np.ascontiguousarray(np.atleast_2d(np.asarray(chain, dtype=np.float64)))
+    lib = _lib.load()
+    pd = rows.ctypes.data_as(C.POINTER(C.c_double))
+    n = C.c_size_t(0)
+    check(lib.olpe_csv_format(pd, rows.shape[0], rows.shape[1], int(nan_row), None, 0,
+                              C.byref(n)))
+    buf = C.create_string_buffer(n.value)
+    check(lib.olpe_csv_format(pd, rows.shape[0], rows.shape[1], int(nan_row), buf, n.value,
+                              C.byref(n)))
+    return buf.raw[:n.value].decode("ascii")
+
+
+def write_chain_csvs(paths, chains, nan_row: bool = True, threads: int = 0) -> None:
+    """Per-walker ``{rank}_finalarray_mpi.csv`` files (apf_step2.py:342-360): file i
+    gets ``chains[i]`` [nrows, PS] after the reference's all-NaN seed row, formatted
+    and written natively from a pool of threads (olpe_csv_write_chains)."""
+    import ctypes as C
+    from . import _lib
+    from ._lib import check
+    chains = np.ascontiguousarray(np.asarray(chains, dtype=np.float64))
+    if chains.ndim != 3 or chains.shape[0] != len(paths):
+        raise ValueError(f"chains must be [len(paths), nrows, ncols], got {chains.shape}")
+    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    check(_lib.load().olpe_csv_write_chains(arr, chains.ctypes.data_as(C.POINTER(C.c_double)),
+                                            len(paths), chains.shape[1], chains.shape[2],
+                                            int(nan_row), int(threads)))
 
 
 def write_chain_csv(path: str, rows) -> None:
-    """``{rank}_finalarray_mpi.csv``: ``rows`` must already hold the NaN seed row."""
-    with open(path, "w", newline="") as f:
-        f.write(format_rows(rows))
+    """One ``{rank}_finalarray_mpi.csv``: ``rows`` must already hold the NaN seed row."""
+    rows = np.atleast_2d(np.asarray(rows, dtype=np.float64))
+    write_chain_csvs([path], rows[None], nan_row=False, threads=1)
 
 
 def with_seed_row(chain):

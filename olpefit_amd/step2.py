@@ -180,15 +180,19 @@ def main(argv=None, nsrc=2, variant="2"):
     for sh in shards:
         chain = sh.chain()
         _, tries, acc = sh.s.get_state()
-        for k in range(sh.W):
-            w = sh.w0 + k
-            if not args.no_csv:
-                chain_name, acc_name = ((f"{w}_finalarray_mpi.csv", f"{w}_acceptance_rate.csv")
-                                        if variant == "2" else
-                                        ("step2a.csv", "step2a_acceptance_rate"))
-                pipeline.write_chain_csv(outdir + chain_name, pipeline.with_seed_row(chain[k]))
+        if not args.no_csv:
+            names = [(f"{sh.w0 + k}_finalarray_mpi.csv", f"{sh.w0 + k}_acceptance_rate.csv")
+                     if variant == "2" else ("step2a.csv", "step2a_acceptance_rate")
+                     for k in range(sh.W)]
+            # chain files: native formatter + writer threads (libolpe olpe_csv_*)
+            # (step 2a names one file for every walker: written in order, the last wins)
+            pipeline.write_chain_csvs([outdir + c for c, _ in names],
+                                      chain.reshape(sh.W, -1, chain.shape[-1]),
+                                      threads=0 if variant == "2" else 1)
+            for k, (_, acc_name) in enumerate(names):
                 pipeline.write_acceptance(outdir + acc_name, acc[k], tries[k])
-            if args.npy:
-                np.save(outdir + f"{w}_chain.npy", chain[k])
+        if args.npy:
+            for k in range(sh.W):
+                np.save(outdir + f"{sh.w0 + k}_chain.npy", chain[k])
     say("done with loop")
     return outdir

@@ -145,3 +145,37 @@ def test_headless_step1_guess(tmp_path):
     assert g[2] == int(p[2] + 1.1) - 11 + xc + 0.5 and g[3] == int(p[3] + 0.4) - 11 + yc + 0.5
     text = open(out[0]).read()
     assert text.endswith("\n") and len(text.split()) == 6
+
+
+def test_native_csv_formatter_equals_repr():
+    """olpe_csv_format (host-only, no GPU) writes what csv.writer writes for float rows
+    (repr of each value): edge values, random magnitudes over 10^+-30, integers, and
+    random bit patterns (subnormals, huge exponents, NaN payloads)."""
+    rs = np.random.RandomState(0)
+    edge = [0.0, -0.0, 1e-5, 1e-4, 1.5e-7, 1e16, 1e15, 1234567890123456.0,
+            12345678901234567.0, np.nan, -np.nan, np.inf, -np.inf, 5e-324,
+            1.7976931348623157e308, 0.1, 1 / 3, 100.0, -2.5, 1e22, 1e-300,
+            9.999999999999999e-5, 0.00010000000000000002]
+    x = np.concatenate([edge, rs.normal(size=30000) * 10.0 ** rs.randint(-30, 30, size=30000),
+                        rs.randint(-10 ** 6, 10 ** 6, size=3000).astype(float),
+                        rs.randint(0, 2 ** 63, size=30000, dtype=np.int64).view(np.float64)])
+    x = x[:len(x) // 7 * 7].reshape(-1, 7)
+    ref = "".join(",".join(repr(v) for v in row) + "\r\n" for row in x.tolist())
+    assert pipeline.format_rows(x) == ref
+    assert pipeline.format_rows(x[:3], nan_row=True) == "nan,nan,nan,nan,nan,nan,nan\r\n" + \
+        "".join(",".join(repr(v) for v in row) + "\r\n" for row in x[:3].tolist())
+
+
+def test_native_chain_writer_threads(tmp_path):
+    """olpe_csv_write_chains: one file per walker from writer threads, bytes equal to
+    the single-file formatter with the NaN seed row; an unwritable path is OLPE_EIO."""
+    from olpefit_amd._lib import OlpeError
+    rs = np.random.RandomState(5)
+    chains = rs.normal(size=(37, 21, 17)) * 1e3
+    paths = [str(tmp_path / f"{w}_finalarray_mpi.csv") for w in range(37)]
+    pipeline.write_chain_csvs(paths, chains, threads=8)
+    for w in (0, 17, 36):
+        with open(paths[w], newline="") as f:
+            assert f.read() == pipeline.format_rows(pipeline.with_seed_row(chains[w]))
+    with pytest.raises(OlpeError):
+        pipeline.write_chain_csvs([str(tmp_path / "no_dir" / "x.csv")], chains[:1])
