@@ -56,7 +56,7 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
     exact: per pixel-Gaussian 7 ops + one exp (E = 20), per pixel G-1 combines +
            background + 3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel, with
-           the RU-row update, 2 sets x (3m-1)/2 (RU = 2) or (5m-1)/4 (RU = 4) (m = nsrc Gaussians per set; G
+           the four-row update, 2 sets x (5m-1)/4 (m = nsrc Gaussians per set; G
            multiplies + G-2 adds per pixel without it) + 2 fma (the two shape tables,
            background folded in) + 2 fma (residual, accumulate); column terms (2 table exps, E_TAB = 12, + 10
            ops per column) only for the Gaussians the drawn parameter changes -- 12 of
@@ -70,10 +70,10 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
     changed = (12 * 2 if nsrc == 2 else (6 * 2 + 2 * 3 + 6 * 3)) / np_
     if n > 64:                       # two column passes: no column-term cache
         changed = g
-    # RU-row update (n >= 64): 2 sets x (3m - 1)/2 per pixel (RU = 2: 2-source 64x64)
-    # or 2 sets x (5m - 1)/4 (RU = 4), + 4; m = nsrc Gaussians per set
+    # four-row update (n >= 64): 2 sets x (5m - 1)/4 per pixel + 4; m = nsrc Gaussians
+    # per set (a 16-wave 2-source sampler, OLPE_WPB=16, uses the two-row one: (3m-1) + 4)
     if n >= 64:
-        per_px = (3 * nsrc - 1) + 4 if (nsrc == 2 and n == 64) else (5 * nsrc - 1) / 2 + 4
+        per_px = (5 * nsrc - 1) / 2 + 4
     else:
         per_px = 2 * g + 2
     return (n * n * per_px + n * changed * (2 * EXP_TAB_OPS + 10)

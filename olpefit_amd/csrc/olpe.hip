@@ -350,7 +350,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       __builtin_amdgcn_s_setprio(0);
       hcache.grp = grp;
       const unsigned gmask = gauss_mask<NSRC>(r);
-      const double part = sweep<NSRC, NT, false, FAST>(*mdl, DE, vtab, nullptr, n, lane, etab,
+      const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask);
       __builtin_amdgcn_s_setprio(1);
       DT_MARK(3);
@@ -619,10 +619,15 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
   if (c->lds_img) {
     switch (c->n) {
       case 32: return launch_gibbs_t<NSRC, 32, true, 16, FAST>(c, a);
-      case 64:
-        if (c->wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
-        if (c->wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
+      case 64: {
+        // FAST: 12 waves per workgroup (168 VGPRs: four-row update and shape-table
+        // prefetch without spills, 3 waves per SIMD with the walker queue keeping them
+        // busy) +1.7 % over 16; EXACT keeps 16
+        const int wpb = c->wpb ? c->wpb : (FAST ? 12 : 16);
+        if (wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
+        if (wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
         return launch_gibbs_t<NSRC, 64, true, 16, FAST>(c, a);
+      }
       default: return launch_gibbs_t<NSRC, 0, true, 16, FAST>(c, a);
     }
   }

@@ -923,7 +923,7 @@ template <int G> struct ColCache {
 #endif
 };
 
-template <int NSRC, int NT, bool WRITE, bool CC = false>
+template <int NSRC, int NT, bool WRITE, bool CC = false, bool WIDE = false>
 __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
                                               const double *htab, double *out, int n_rt,
                                               int lane, int rows, int kc, ExpTab ex,
@@ -996,17 +996,27 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       }
     };
     // RU rows per update (the unrolled row loop): row k+r sums a_k rho^r (r < RU)
-    // with fmas and a_(k+RU) = a_k rho^RU.  Per set of m Gaussians: RU = 2 costs 3m-1
-    // operations per two rows (9 FP64 per pixel for two sources), RU = 4 5m-1 per four
-    // rows (8.5), against 2m-1 per row without it (10).  RU = 2 for the 2-source 64x64
-    // sampler: with the walker queue it spilled less (16 VGPRs fewer for the powers),
-    // 518 vs 502 M walker-steps/s on one box; RU = 4 elsewhere (3-source 128x128: 88.2
-    // vs 85.7 M).  The powers are formed once per column; the recurrence rounds n/RU
-    // times down a column.
+    // with fmas and a_(k+RU) = a_k rho^RU.  Per set of m Gaussians: RU = 4 costs 5m-1
+    // operations per four rows (8.5 FP64 per pixel for two sources), RU = 2 3m-1 per
+    // two rows (9), against 2m-1 per row without it (10).  RU = 2 only where registers
+    // are short (LEAN below: with the walker queue it spilled less, 518 vs 502 M
+    // walker-steps/s on one box); the 12-wave sampler runs RU = 4 with the prefetch
+    // (510 vs 500 M against the 16-wave LEAN one; 3-source 128x128: 88.2 vs 85.7 M).
+    // The powers are formed once per column; the recurrence rounds n/RU times down a
+    // column.
+    // LEAN: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): two-row
+    // update and no shape-table prefetch; with 12 waves (WIDE, 168 VGPRs) and
+    // elsewhere the four-row update with the prefetch
+    constexpr bool LEAN = NSRC == 2 && NT == 64 && !WIDE;
 #ifdef OLPE_ROWU
     constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
 #else
-    constexpr int RU = (NSRC == 2 && NT == 64) ? 2 : 4;
+    constexpr int RU = LEAN ? 2 : 4;
+#endif
+#ifdef OLPE_H_PREFETCH
+    constexpr bool HPF = OLPE_H_PREFETCH;
+#else
+    constexpr bool HPF = !LEAN;
 #endif
     double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
 #pragma unroll
@@ -1053,34 +1063,34 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       const int rstep = cw.S * n;
       const double2 *p = DW + cw.grp * n + jj;
       double2 cur[BLK], nxt[BLK];
-#ifndef OLPE_H_PREFETCH
-      // the shape-table rows (wave-uniform broadcast reads) are read with their block;
-      // only the cutout rows are prefetched a block ahead (16 VGPRs fewer)
-      double2 hc[BLK];
+      if constexpr (!HPF) {
+        // the shape-table rows (wave-uniform broadcast reads) are read with their block;
+        // only the cutout rows are prefetched a block ahead (16 VGPRs fewer)
+        double2 hc[BLK];
 #pragma unroll
-      for (int k = 0; k < BLK; ++k) cur[k] = p[k * rstep];
-      const int R = NT >= 64 ? NT : rows;
+        for (int k = 0; k < BLK; ++k) cur[k] = p[k * rstep];
+        const int R = NT >= 64 ? NT : rows;
 #pragma unroll 16
-      for (int b0 = 0; b0 < R; b0 += BLK) {
-        const bool more = b0 + BLK < R;
-        const double2 *pn = p + (more ? BLK * rstep : 0);
+        for (int b0 = 0; b0 < R; b0 += BLK) {
+          const bool more = b0 + BLK < R;
+          const double2 *pn = p + (more ? BLK * rstep : 0);
+#pragma unroll
+          for (int k = 0; k < BLK; ++k) {
+            hc[k] = hr[b0 + k];
+            nxt[k] = pn[k * rstep];
+          }
+#pragma unroll
+          for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
+#pragma unroll
+          for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+          p = pn;
+        }
+      } else {
+        double2 hc[BLK], hn[BLK];
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
-          hc[k] = hr[b0 + k];
-          nxt[k] = pn[k * rstep];
-        }
-#pragma unroll
-        for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
-#pragma unroll
-        for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
-        p = pn;
-      }
-#else
-      double2 hc[BLK], hn[BLK];
-#pragma unroll
-      for (int k = 0; k < BLK; ++k) {
-        cur[k] = p[k * rstep];
-        hc[k] = hr[k];
+          cur[k] = p[k * rstep];
+          hc[k] = hr[k];
       }
       // n >= 64 (S = 1): rows = n is a compile-time count and the row loop is unrolled
       // (every LDS address an immediate offset, no loop counter): +3.6 %
@@ -1104,7 +1114,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         }
         p = pn;
       }
-#endif
+      }
     } else {
       int k = 0;
 #pragma unroll 2
@@ -1149,7 +1159,7 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
   cc.pend = 0;
 }
 
-template <int NSRC, int NT, bool WRITE, bool FAST>
+template <int NSRC, int NT, bool WRITE, bool FAST, bool WIDE = false>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane,
                                         const double *etab, HCache *hc = nullptr,
@@ -1206,10 +1216,10 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       asm volatile("" ::: "memory");
       if constexpr (NT != 0 && NT <= 64) {
         if (cc)
-          return sweep_fast3<NSRC, NT, WRITE, true>(m, img, h, out, n, lane, rows, kc,
+          return sweep_fast3<NSRC, NT, WRITE, true, WIDE>(m, img, h, out, n, lane, rows, kc,
                                                     ExpTab{etab}, cc, gmask);
       }
-      return sweep_fast3<NSRC, NT, WRITE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
+      return sweep_fast3<NSRC, NT, WRITE, false, WIDE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
     }
     const int lvl = fast_level<NSRC>(m, nn);
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
