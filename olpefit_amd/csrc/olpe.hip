@@ -360,7 +360,11 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       // accept_reject (:139-148)
       // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
       const double la = -(chi - st[PS - 1]) / 2.;
+#ifdef OLPE_DIAG_NO_ACCEPT_EXP
+      const double p_accept = 1.0 + la;           // diagnostic: accept test without exp
+#else
       const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
+#endif
       const double dice = drawtab[dice_idx];
       const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
       hcache.after(acc);

@@ -923,12 +923,52 @@ template <int G> struct ColCache {
 #endif
 };
 
+// The proposal's column terms of the Gaussians it moves (gauss_mask: 0, 2 or NSRC of
+// them), lane = column of a single-pass sweep (n <= 64), in one straight-line block so
+// that their independent exp chains interleave with each other and with the guard,
+// which runs after it: the setup is latency-bound (a diagnostic build without column
+// terms runs 25 % faster, for ~10 % of the VALU instructions).  One Gaussian per
+// branch inside the sweep (OLPE_COLTERM_SERIAL) was 1.2 % slower; raised priority
+// for the block gained nothing.
+template <int NSRC> struct MovedTerms {
+  double E[NSRC], R[NSRC];   // component-wise: struct selects go through scratch
+  int gi[NSRC];              // Gaussian of slot k (-1: none)
+  int nm;                    // moved Gaussians
+};
+
+template <int NSRC>
+__device__ __forceinline__ void moved_terms(MovedTerms<NSRC> &mt, const ModelDesc<NSRC> &m,
+                                            unsigned gmask, int n, int lane, int kc,
+                                            ExpTab ex) {
+  const ColWalk cw(n, lane);
+  mt.nm = __builtin_popcount(gmask);
+  unsigned rest = gmask;
+#pragma unroll
+  for (int k = 0; k < NSRC; ++k) {
+    mt.gi[k] = rest ? __builtin_ctz(rest) : -1;
+    rest &= rest - 1u;
+  }
+#ifndef OLPE_DIAG_NO_COLTERM
+  if (mt.nm >= 2) {
+    // (two moved with three sources: the third term repeats the first one)
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) {
+      const ColTerm t = col_term(m.g[k < mt.nm ? mt.gi[k] : mt.gi[0]], (double)cw.jl,
+                                 (double)cw.grp, (double)cw.S, (double)kc, ex);
+      mt.E[k] = t.E;
+      mt.R[k] = t.R;
+    }
+  }
+#endif
+}
+
 template <int NSRC, int NT, bool WRITE, bool CC = false, bool WIDE = false>
 __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const double2 *DW,
                                               const double *htab, double *out, int n_rt,
                                               int lane, int rows, int kc, ExpTab ex,
                                               ColCache<2 * NSRC> *cc = nullptr,
-                                              unsigned gmask = 0) {
+                                              unsigned gmask = 0,
+                                              const MovedTerms<NSRC> *pre = nullptr) {
   constexpr int G = 2 * NSRC;
   const int n = NT ? NT : n_rt;
   const ColWalk cw(n, lane);
@@ -942,16 +982,58 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     const bool act = cw.lane_ok && j < n;
     const double xj = (double)j;
     double av[G], rho[G];
+#ifndef OLPE_COLTERM_SERIAL
+    // the moved Gaussians' terms come precomputed (moved_terms, before the guard)
+    if constexpr (CC) {
+#ifndef OLPE_DIAG_NO_COLTERM
+      if (pre->nm >= 2) {
+#ifdef OLPE_DIAG_TIMING
+        cc->n_setup += pre->nm;
+#endif
+        if (cc->pbuf) {          // park the proposal's terms for an accept
+#pragma unroll
+          for (int k = 0; k < NSRC; ++k) {
+            if (k < pre->nm) {
+              cc->pbuf[(2 * k) * 64 + lane] = pre->E[k];
+              cc->pbuf[(2 * k + 1) * 64 + lane] = pre->R[k];
+            }
+          }
+        }
+      }
+#endif
+    }
+#endif
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       ColTerm t;
       if constexpr (CC) {
         const bool mine = (gmask >> g) & 1u;
+#ifndef OLPE_COLTERM_SERIAL
 #ifdef OLPE_DIAG_NO_COLTERM
         if (true) {                              // diagnostic: column terms never recomputed
 #else
-        if (((cc->valid >> g) & 1u) && !mine) {
+        if (mine) {
+          double e = pre->E[0], r = pre->R[0];
+#pragma unroll
+          for (int k = 1; k < NSRC; ++k) {
+            e = (g == pre->gi[k]) ? pre->E[k] : e;
+            r = (g == pre->gi[k]) ? pre->R[k] : r;
+          }
+          t = ColTerm{e, r};
+        } else if ((cc->valid >> g) & 1u) {
 #endif
+          t = ColTerm{cc->E[g], cc->R[g]};
+        } else {                 // (first step of a walker) a term of the current state
+          t = col_term(m.g[g], xj, yr, S, kcd, ex);
+#ifdef OLPE_DIAG_TIMING
+          ++cc->n_setup;
+#endif
+          cc->E[g] = t.E;
+          cc->R[g] = t.R;
+          cc->valid |= 1u << g;
+        }
+#else
+        if (((cc->valid >> g) & 1u) && !mine) {
           t = ColTerm{cc->E[g], cc->R[g]};
         } else {
           t = col_term(m.g[g], xj, yr, S, kcd, ex);
@@ -968,6 +1050,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
             cc->pbuf[(2 * slot + 1) * 64 + lane] = t.R;
           }
         }
+#endif
       } else {
         t = col_term(m.g[g], xj, yr, S, kcd, ex);
       }
@@ -1179,6 +1262,10 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     const int rows = (nn - cw.grp + cw.S - 1) / cw.S;    // uniform when S divides n
     const int rows0 = (nn + cw.S - 1) / cw.S;             // rows of row group 0 (most)
     const int kc = rows0 / 2;
+    // the moved Gaussians' column terms first: their exp chains and the guard's form
+    // one scheduling region (single-pass sampler kernels, which always pass cc)
+    MovedTerms<NSRC> pre;
+    if constexpr (NT != 0 && NT <= 64) moved_terms<NSRC>(pre, m, gmask, nn, lane, kc, ExpTab{etab});
 #ifdef OLPE_DIAG_NO_GUARD
     const bool ok3 = true;                       // diagnostic: guard skipped
 #else
@@ -1217,7 +1304,7 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       if constexpr (NT != 0 && NT <= 64) {
         if (cc)
           return sweep_fast3<NSRC, NT, WRITE, true, WIDE>(m, img, h, out, n, lane, rows, kc,
-                                                    ExpTab{etab}, cc, gmask);
+                                                          ExpTab{etab}, cc, gmask, &pre);
       }
       return sweep_fast3<NSRC, NT, WRITE, false, WIDE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
     }
