@@ -357,16 +357,19 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       const double chi = wave_sum(part);
       DT_MARK(4);
 
-      // accept_reject (:139-148)
-      // FAST kernels: the table exp (<= 1.13 ulp; NaN kept so that NaN chi^2 rejects)
-      const double la = -(chi - st[PS - 1]) / 2.;
-#ifdef OLPE_DIAG_NO_ACCEPT_EXP
-      const double p_accept = 1.0 + la;           // diagnostic: accept test without exp
-#else
-      const double p_accept = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);
-#endif
+      // accept_reject (:139-148): EXACT dice < exp(-(chi - cur)/2); FAST the same test
+      // as chi - cur < -2 log(dice) against the batch's threshold table (a NaN chi^2
+      // rejects in both)
+      const double dchi = chi - st[PS - 1];
+      const double la = -dchi / 2.;
       const double dice = drawtab[dice_idx];
-      const bool acc = __builtin_amdgcn_readfirstlane(dice < p_accept ? 1 : 0) != 0;
+      bool acc;
+      if constexpr (FAST) {
+        const double thr = drawtab[kThr + (dice_idx == 128 ? 64 : dice_idx)];
+        acc = __builtin_amdgcn_readfirstlane(dchi < thr ? 1 : 0) != 0;
+      } else {
+        acc = __builtin_amdgcn_readfirstlane(dice < exp(la) ? 1 : 0) != 0;
+      }
       hcache.after(acc);
       if constexpr (FAST && NT != 0 && NT <= 64) {
 #ifndef OLPE_DIAG_NO_REFRESH
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
         t[1] = nv;
         t[2] = chi;
         t[3] = dice;
-        t[4] = p_accept;
+        t[4] = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);   // p_accept
         t[5] = acc ? 1.0 : 0.0;
       }
 #endif
@@ -624,10 +627,11 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
     switch (c->n) {
       case 32: return launch_gibbs_t<NSRC, 32, true, 16, FAST>(c, a);
       case 64: {
-        // FAST: 12 waves per workgroup (168 VGPRs: four-row update and shape-table
-        // prefetch without spills, 3 waves per SIMD with the walker queue keeping them
-        // busy) +1.7 % over 16; EXACT keeps 16
-        const int wpb = c->wpb ? c->wpb : (FAST ? 12 : 16);
+        // 12 waves per workgroup (168 VGPRs: four-row update and shape-table prefetch
+        // without spills, 3 waves per SIMD with the walker queue keeping them busy):
+        // FAST +1.7 % over 16, EXACT the same; 16 would not fit the LDS beside the
+        // draw tables' accept thresholds
+        const int wpb = c->wpb ? c->wpb : 12;
         if (wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
         if (wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
         return launch_gibbs_t<NSRC, 64, true, 16, FAST>(c, a);
@@ -715,8 +719,10 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->np = nsrc == 2 ? 16 : 19;
   c->ps = c->np + 1;
   const size_t npix = (size_t)nx * nx;
-  // stage image + 1/err in LDS when it fits beside 16 walkers' RNG state
-  c->lds_img = npix * sizeof(double2) + 16 * wave_lds(nx, c->np, true) + kEtabBytes <= 160 * 1024;
+  // stage image + 1/err in LDS when it fits beside a workgroup's wave slices (12 waves
+  // at 64x64, 16 otherwise; launch_gibbs_m)
+  c->lds_img = npix * sizeof(double2) + (nx == 64 ? 12 : 16) * wave_lds(nx, c->np, true) +
+                   kEtabBytes <= 160 * 1024;
   if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
   std::vector<double2> hDE(npix), hDW(npix);

@@ -167,6 +167,18 @@ __device__ inline uint32_t mt_twist(uint32_t *gkey, int lane) {
   return k[0];
 }
 
+// Accept test of FAST kernels: the reference accepts when dice < exp(-d/2), d = the
+// chi^2 increase (apf_step2.py:139-148); for dice in [0, 1) that is d < -2 log(dice),
+// so the threshold of every rand() of a batch is prepared lane-parallel with the draw
+// tables (one log per 64 words) and the accept is one compare instead of an exp per
+// step.  The two forms can only disagree where d and -2 log(dice) agree to rounding
+// (the tests' flip criterion).  dice = 0 accepts below d = 1490.27, where exp(-d/2)
+// underflows to 0 and the reference rejects.
+__device__ __forceinline__ double accept_threshold(double u) {
+  return u > 0.0 ? -2.0 * log(u) : 1490.2664382038824;
+}
+constexpr int kThr = 129;       // MTWave::tab offset of the accept thresholds
+
 struct MTWave {
   uint32_t *key;  // HBM, MT_N words (this walker's row)
   int pos;        // numpy state->pos (uniform)
@@ -178,7 +190,8 @@ struct MTWave {
   // per-batch draw tables (LDS, kDrawTab doubles per wave): tab[l] = rand() of words
   // (l, l+1), tab[64 + l] = polar factor sqrt(-2 log r2 / r2) of the attempt at word
   // l, or -1 where that attempt is rejected (l + 3 < bsize), tab[128] = a rand()
-  // assembled across the key end
+  // assembled across the key end; tab[kThr + i] = accept threshold of the rand() at
+  // tab[i] (i = 0..63, and 64 for tab[128]): -2 log(u), see accept_threshold
   double *tab;
 
   // load the batch [pos, pos + 64) of the key (at most to its end; a used-up key is
@@ -214,6 +227,7 @@ struct MTWave {
     const double f = sqrt(-2.0 * log(r2) / r2);
     tab[lane] = u;
     tab[64 + lane] = ((r2 < 1.0) & (r2 != 0.0)) ? f : -1.0;   // bitwise &: no branches
+    tab[kThr + lane] = accept_threshold(u);
     wave_sync();
   }
 
@@ -325,7 +339,11 @@ struct MTWave {
           has_gauss = 1;
           g = uniform_f64(f * x2);
         } else {
-          if (lane == 0) tab[128] = ((double)(w2 >> 5) * 67108864.0 + (double)(w3 >> 6)) / 9007199254740992.0;
+          if (lane == 0) {
+            const double u = ((double)(w2 >> 5) * 67108864.0 + (double)(w3 >> 6)) / 9007199254740992.0;
+            tab[128] = u;
+            tab[kThr + 64] = accept_threshold(u);
+          }
           wave_sync();
           dice_idx = 128;
         }
@@ -343,7 +361,7 @@ struct MTWave {
     return v;
   }
 };
-constexpr int kDrawTab = 129;   // doubles of MTWave::tab
+constexpr int kDrawTab = kThr + 65;   // doubles of MTWave::tab
 
 // np.random.seed(s): init_genrand (mt19937_seed)
 __device__ inline void mt_seed_serial(uint32_t *key, uint32_t s) {

@@ -12,7 +12,7 @@ struct olpe_ctx {
   int np = 16, ps = 17;
   int eval_mode = 1;   // OLPE_EVAL_FAST (default) / OLPE_EVAL_EXACT
   bool lds_img = true; // cutout + 1/err staged in LDS by the sampler
-  int wpb = 0;         // waves per workgroup of the 64x64 LDS sampler (0 = 12 FAST, 16 EXACT)
+  int wpb = 0;         // waves per workgroup of the 64x64 LDS sampler (0 = 12)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
