@@ -103,7 +103,8 @@ template <int NP> struct WaveSlice {
   static constexpr int OPT = PS + 12, OPC = PS + 15;
   static constexpr int F64 = PS + 18;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
-  static constexpr int OPE = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
+  static constexpr int OCC = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;  // col_coef [G][3]
+  static constexpr int OPE = (OCC + 2 * NSRC * 3 * 8 + 15) & ~15;
   static constexpr int BYTES = OPE + NSRC * 2 * 64 * 8;
 };
 // MTWave draw tables (kDrawTab doubles per wave).  Kernels with the FAST3 column-term
@@ -157,6 +158,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
   double *vtab = reinterpret_cast<double *>(wb + WS::BYTES + TABX);
   double *drawtab = reinterpret_cast<double *>(wb + (TABX ? WS::BYTES : WS::OPE));
   ModelDesc<NSRC> *mdl = reinterpret_cast<ModelDesc<NSRC> *>(wb + WS::OMD);
+  double *colc = reinterpret_cast<double *>(wb + WS::OCC);
 
   if constexpr (LDS_IMG) {
     // one coalesced 16-B-per-lane staging pass of {data, 1/err}
@@ -242,6 +244,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     HCache hcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
+    ccache.colc = colc;
 #pragma unroll
     for (int g = 0; g < 2 * NSRC; ++g) ccache.E[g] = ccache.R[g] = 0.0;
     __builtin_amdgcn_s_setprio(1);
@@ -336,8 +339,11 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
         // component-wise selects (a select of whole structs goes through scratch)
         const Coef C{narrow ? C1p.a : C2p.a, narrow ? C1p.b : C2p.b, narrow ? C1p.c : C2p.c};
         const double dx = narrow ? 0.0 : ql(L::DX), dy = narrow ? 0.0 : ql(L::DY);
-        mdl->g[lane] = Gauss{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
-                             narrow ? yc : yc + dy, C};
+        const Gauss gq{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
+                       narrow ? yc : yc + dy, C};
+        mdl->g[lane] = gq;
+        // n = 64 FAST sweeps: the column-term coefficients of this Gaussian (col_term64)
+        if constexpr (FAST && NT == 64) col_coef(gq, (double)(NT / 2), colc + 3 * lane);
       } else if (lane == 2 * NSRC) {
         mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
       }

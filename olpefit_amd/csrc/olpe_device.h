@@ -909,6 +909,23 @@ __device__ __forceinline__ ColTerm col_term(const Gauss &q, double xj, double yr
   return ColTerm{ex(-(q0 - cs * (kcd * (kcd + 1.0)))), ex(-(d0 + 2.0 * cs * kcd))};
 }
 
+// The same terms for a single-pass sweep with S = 1 and row group 0 (n = 64), from
+// per-step coefficients prepared lane-parallel with the descriptor (col_coef):
+// q0 - K = (a xd + beta) xd + gamma and the rho exponent b xd + delta -- 3 fma per
+// column-Gaussian instead of ~11 operations (the column terms' setup is on the step's
+// critical path).  Every cached and refreshed term of such a sweep uses this form.
+__device__ __forceinline__ void col_coef(const Gauss &q, double kcd, double *cc) {
+  const double yd = -q.y0;
+  cc[0] = q.k.b * yd;
+  cc[1] = q.k.c * (yd * yd - kcd * (kcd + 1.0));
+  cc[2] = q.k.c * ((2.0 * yd + 1.0) + 2.0 * kcd);
+}
+__device__ __forceinline__ ColTerm col_term64(const Gauss &q, const double *cc, double xj,
+                                              ExpTab ex) {
+  const double xd = xj - q.x0;
+  return ColTerm{ex(-fma(fma(q.k.a, xd, cc[0]), xd, cc[1])), ex(-fma(q.k.b, xd, cc[2]))};
+}
+
 // Gaussians whose column terms a proposal of parameter r changes (bit g): a source's
 // position moves its two Gaussians, DX/DY the wide ones, a shape set its own; the
 // amplitudes, ratio, offset and background change no E or rho.
@@ -936,6 +953,8 @@ template <int G> struct ColCache {
   // recomputing (pend = the gmask they belong to)
   double *pbuf = nullptr;
   unsigned pend = 0;
+  // the step's col_coef coefficients [G][3] (LDS), for n = 64 sweeps (col_term64)
+  const double *colc = nullptr;
 #ifdef OLPE_DIAG_TIMING
   unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
 #endif
@@ -946,18 +965,18 @@ template <int G> struct ColCache {
 // that their independent exp chains interleave with each other and with the guard,
 // which runs after it: the setup is latency-bound (a diagnostic build without column
 // terms runs 25 % faster, for ~10 % of the VALU instructions).  One Gaussian per
-// branch inside the sweep (OLPE_COLTERM_SERIAL) was 1.2 % slower; raised priority
-// for the block gained nothing.
+// branch inside the sweep was 0.3-1.2 % slower; raised priority for the block
+// gained nothing.
 template <int NSRC> struct MovedTerms {
   double E[NSRC], R[NSRC];   // component-wise: struct selects go through scratch
   int gi[NSRC];              // Gaussian of slot k (-1: none)
   int nm;                    // moved Gaussians
 };
 
-template <int NSRC>
+template <int NSRC, int NT>
 __device__ __forceinline__ void moved_terms(MovedTerms<NSRC> &mt, const ModelDesc<NSRC> &m,
                                             unsigned gmask, int n, int lane, int kc,
-                                            ExpTab ex) {
+                                            ExpTab ex, const double *colc) {
   const ColWalk cw(n, lane);
   mt.nm = __builtin_popcount(gmask);
   unsigned rest = gmask;
@@ -971,8 +990,12 @@ __device__ __forceinline__ void moved_terms(MovedTerms<NSRC> &mt, const ModelDes
     // (two moved with three sources: the third term repeats the first one)
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) {
-      const ColTerm t = col_term(m.g[k < mt.nm ? mt.gi[k] : mt.gi[0]], (double)cw.jl,
-                                 (double)cw.grp, (double)cw.S, (double)kc, ex);
+      const int g = k < mt.nm ? mt.gi[k] : mt.gi[0];
+      ColTerm t;
+      if constexpr (NT == 64)
+        t = col_term64(m.g[g], colc + 3 * g, (double)cw.jl, ex);
+      else
+        t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S, (double)kc, ex);
       mt.E[k] = t.E;
       mt.R[k] = t.R;
     }
@@ -1000,7 +1023,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     const bool act = cw.lane_ok && j < n;
     const double xj = (double)j;
     double av[G], rho[G];
-#ifndef OLPE_COLTERM_SERIAL
     // the moved Gaussians' terms come precomputed (moved_terms, before the guard)
     if constexpr (CC) {
 #ifndef OLPE_DIAG_NO_COLTERM
@@ -1020,13 +1042,11 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
       }
 #endif
     }
-#endif
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       ColTerm t;
       if constexpr (CC) {
         const bool mine = (gmask >> g) & 1u;
-#ifndef OLPE_COLTERM_SERIAL
 #ifdef OLPE_DIAG_NO_COLTERM
         if (true) {                              // diagnostic: column terms never recomputed
 #else
@@ -1042,7 +1062,10 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 #endif
           t = ColTerm{cc->E[g], cc->R[g]};
         } else {                 // (first step of a walker) a term of the current state
-          t = col_term(m.g[g], xj, yr, S, kcd, ex);
+          if constexpr (NT == 64)
+            t = col_term64(m.g[g], cc->colc + 3 * g, xj, ex);
+          else
+            t = col_term(m.g[g], xj, yr, S, kcd, ex);
 #ifdef OLPE_DIAG_TIMING
           ++cc->n_setup;
 #endif
@@ -1050,25 +1073,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           cc->R[g] = t.R;
           cc->valid |= 1u << g;
         }
-#else
-        if (((cc->valid >> g) & 1u) && !mine) {
-          t = ColTerm{cc->E[g], cc->R[g]};
-        } else {
-          t = col_term(m.g[g], xj, yr, S, kcd, ex);
-#ifdef OLPE_DIAG_TIMING
-          ++cc->n_setup;
-#endif
-          if (!mine) {           // unchanged by the proposal: a term of the current state
-            cc->E[g] = t.E;
-            cc->R[g] = t.R;
-            cc->valid |= 1u << g;
-          } else if (cc->pbuf) { // moved: park the proposal's terms for an accept
-            const int slot = __builtin_popcount(gmask & ((1u << g) - 1u));
-            cc->pbuf[(2 * slot) * 64 + lane] = t.E;
-            cc->pbuf[(2 * slot + 1) * 64 + lane] = t.R;
-          }
-        }
-#endif
       } else {
         t = col_term(m.g[g], xj, yr, S, kcd, ex);
       }
@@ -1249,8 +1253,11 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
 #ifdef OLPE_DIAG_TIMING
         ++cc.n_refresh;
 #endif
-        const ColTerm t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S,
-                                   kcd, ExpTab{etab});
+        ColTerm t;
+        if constexpr (NT == 64)
+          t = col_term64(m.g[g], cc.colc + 3 * g, (double)cw.jl, ExpTab{etab});
+        else
+          t = col_term(m.g[g], (double)cw.jl, (double)cw.grp, (double)cw.S, kcd, ExpTab{etab});
         cc.E[g] = t.E;
         cc.R[g] = t.R;
       }
@@ -1283,7 +1290,8 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     // the moved Gaussians' column terms first: their exp chains and the guard's form
     // one scheduling region (single-pass sampler kernels, which always pass cc)
     MovedTerms<NSRC> pre;
-    if constexpr (NT != 0 && NT <= 64) moved_terms<NSRC>(pre, m, gmask, nn, lane, kc, ExpTab{etab});
+    if constexpr (NT != 0 && NT <= 64)
+      moved_terms<NSRC, NT>(pre, m, gmask, nn, lane, kc, ExpTab{etab}, cc->colc);
 #ifdef OLPE_DIAG_NO_GUARD
     const bool ok3 = true;                       // diagnostic: guard skipped
 #else
