@@ -342,8 +342,9 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
         const Gauss gq{narrow ? tot - wide : wide, narrow ? xc : xc + dx,
                        narrow ? yc : yc + dy, C};
         mdl->g[lane] = gq;
-        // n = 64 FAST sweeps: the column-term coefficients of this Gaussian (col_term64)
-        if constexpr (FAST && NT == 64) col_coef(gq, (double)(NT / 2), colc + 3 * lane);
+        // FAST sweeps of n = 64 / 128: the column-term coefficients of this Gaussian
+        // (col_term64, row group 0 and S = 1 in both)
+        if constexpr (FAST && NT >= 64) col_coef(gq, (double)(NT / 2), colc + 3 * lane);
       } else if (lane == 2 * NSRC) {
         mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
       }

@@ -909,7 +909,7 @@ __device__ __forceinline__ ColTerm col_term(const Gauss &q, double xj, double yr
   return ColTerm{ex(-(q0 - cs * (kcd * (kcd + 1.0)))), ex(-(d0 + 2.0 * cs * kcd))};
 }
 
-// The same terms for a single-pass sweep with S = 1 and row group 0 (n = 64), from
+// The same terms for sweeps with S = 1 and row group 0 (n = 64 and 128), from
 // per-step coefficients prepared lane-parallel with the descriptor (col_coef):
 // q0 - K = (a xd + beta) xd + gamma and the rho exponent b xd + delta -- 3 fma per
 // column-Gaussian instead of ~11 operations (the column terms' setup is on the step's
@@ -953,7 +953,7 @@ template <int G> struct ColCache {
   // recomputing (pend = the gmask they belong to)
   double *pbuf = nullptr;
   unsigned pend = 0;
-  // the step's col_coef coefficients [G][3] (LDS), for n = 64 sweeps (col_term64)
+  // the step's col_coef coefficients [G][3] (LDS), for n = 64 / 128 sweeps (col_term64)
   const double *colc = nullptr;
 #ifdef OLPE_DIAG_TIMING
   unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
@@ -1073,6 +1073,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           cc->R[g] = t.R;
           cc->valid |= 1u << g;
         }
+      } else if constexpr (NT >= 64) {      // sampler kernels (cc carries the coefficients)
+        t = col_term64(m.g[g], cc->colc + 3 * g, xj, ex);
       } else {
         t = col_term(m.g[g], xj, yr, S, kcd, ex);
       }
@@ -1332,7 +1334,8 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
           return sweep_fast3<NSRC, NT, WRITE, true, WIDE>(m, img, h, out, n, lane, rows, kc,
                                                           ExpTab{etab}, cc, gmask, &pre);
       }
-      return sweep_fast3<NSRC, NT, WRITE, false, WIDE>(m, img, h, out, n, lane, rows, kc, ExpTab{etab});
+      return sweep_fast3<NSRC, NT, WRITE, false, WIDE>(m, img, h, out, n, lane, rows, kc,
+                                                       ExpTab{etab}, cc);
     }
     const int lvl = fast_level<NSRC>(m, nn);
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
