@@ -806,6 +806,24 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
                   (int)(q.k.c >= 0.0);
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
+// The same test, returning the Gaussians that fail it (bit g), for the per-column
+// guard to retest only those.
+template <int NSRC>
+__device__ __forceinline__ unsigned fast3_fails(const ModelDesc<NSRC> &m, int n, int rows,
+                                                int kc, int lane) {
+  const double hi = (double)(n - 1);
+  const double S2 = (double)(row_stride(n) * row_stride(n));
+  const double km = (double)(kc > rows - 1 - kc ? kc : rows - 1 - kc) + 1.0;
+  const Gauss &q = m.g[lane < 2 * NSRC ? lane : 0];
+  const double mx = fmax(fabs(q.x0), fabs(hi - q.x0));
+  const double my = fmax(fabs(q.y0), fabs(hi - q.y0));
+  const double Qb = (q.k.a * (mx * mx) + fabs(q.k.b) * mx * my) + q.k.c * (my * my);
+  const double cs = q.k.c * S2;
+  const bool ok = (int)(cs * km * km < 600.0) & (int)(Qb < 700.0 + cs * kc * (kc + 1.0)) &
+                  (int)isfinite(Qb) & (int)isfinite(q.amp) & (int)(q.k.a >= 0.0) &
+                  (int)(q.k.c >= 0.0);
+  return (unsigned)__builtin_amdgcn_ballot_w64(!ok) & ((1u << (2 * NSRC)) - 1u);
+}
 
 // FAST3 guard, per column (when fast3_ok's whole-grid bound fails, e.g. a source far
 // from the grid centre of a 128-pixel cutout, where Q over the whole grid exceeds the
@@ -820,7 +838,7 @@ __device__ __forceinline__ bool fast3_ok(const ModelDesc<NSRC> &m, int n, int ro
 // |A| < 1e20 keeps A e^-100 negligible beside any model value.
 template <int NSRC>
 __device__ __forceinline__ bool fast3_ok_cols(const ModelDesc<NSRC> &m, int n, int rows, int kc,
-                                              int lane) {
+                                              int lane, unsigned which) {
   const ColWalk cw(n, lane);
   const double S = (double)cw.S;
   const double kcd = (double)kc;
@@ -830,8 +848,8 @@ __device__ __forceinline__ bool fast3_ok_cols(const ModelDesc<NSRC> &m, int n, i
   // not unrolled: the descriptor is in LDS, and the guard must not raise the sampler's
   // register pressure (an unrolled form spilled)
 #pragma unroll 1
-  for (int g = 0; g < 2 * NSRC; ++g) {
-    const Gauss &q = m.g[g];
+  for (unsigned f = which; f; f &= f - 1u) {
+    const Gauss &q = m.g[__builtin_ctz(f)];
     const double cs = q.k.c * (S * S);
     const double K = cs * (kcd * (kcd + 1.0));
     const double amin = q.k.a - (q.k.b * q.k.b) / (4.0 * q.k.c);
@@ -1297,15 +1315,20 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
 #ifdef OLPE_DIAG_NO_GUARD
     const bool ok3 = true;                       // diagnostic: guard skipped
 #else
-    bool ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+    bool ok3;
     // the per-column guard only where the whole-grid one can fail on a well-placed
-    // model (cutouts wider than 64 columns); at n <= 64 it would cost the sampler
-    // registers for a branch the bench never takes
+    // model (cutouts wider than 64 columns), and only for the Gaussians that failed
+    // it (the 3-source 128x128 bench model: 2 of 6); at n <= 64 it would cost the
+    // sampler registers for a branch the bench never takes
     if constexpr (NT == 0 || NT > 64) {
+      const unsigned fails = fast3_fails<NSRC>(m, nn, rows0, kc, lane);
+      ok3 = fails == 0;
       if (!ok3) {
         asm volatile("" ::: "memory");
-        ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane);
+        ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane, fails);
       }
+    } else {
+      ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
     }
 #endif
     asm volatile("" ::: "memory");
