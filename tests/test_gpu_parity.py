@@ -418,3 +418,31 @@ def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
     for w, sd in enumerate(seeds):
         ref, _ = ora.Walker(dm, err, p0, sd, nsrc=nsrc).run(300, record_stride=2)
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+
+
+@pytest.mark.parametrize("core", [(0.3, 0.3, 0.0), (0.3, 0.5, 0.7), (0.6, 0.45, -0.4)])
+def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core):
+    """A tiny narrow core (sigma 0.3-0.6 px) fails the FAST3 guard (c S^2 (kc+1)^2 >=
+    600), so the sampler's steps take the fallback sweeps inside the 64x64 kernel: the
+    V-table (circular core, b = 0) or the exact per-pixel sweep (elongated, rotated
+    core), interleaved with FAST3 steps when a proposal widens the core; the shape-table
+    cache is invalidated when the V table overwrites it.  3 walkers x 400 iterations
+    against the oracle at the FAST tolerance."""
+    g = golden("c64")
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    p0 = g["p_init"].copy()
+    p0[10], p0[11], p0[14] = core
+    with np.errstate(all="ignore"):
+        p0[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p0, 64), err))
+    s = make_sampler(g, "fast")
+    assert abs(s.chi_squared(p0) - p0[-1]) <= TOL["fast"]["chi"] * p0[-1]
+    seeds = [41, 42, 43]
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (3, 1)))
+    s.enable_trace(True)
+    chain = s.run(400, burn_in=0, record_stride=1)
+    tr = s.trace(400)
+    for w, sd in enumerate(seeds):
+        ref, rtr = ora.Walker(dm, err, p0, sd).run(400, trace=True)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
+        assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
