@@ -1,11 +1,13 @@
 // olpe.hip -- gfx950 kernels and the C-ABI (include/olpe.h) of libolpe.so.
 //
 // Kernels
-//   olpe_gibbs_kernel  fused sampler: W walkers, one per wavefront, n_iters Gibbs
-//                      iterations each (apf_step2.py:300-351) with the cutout and
-//                      inverse-sigma map staged once per workgroup into LDS.
-//   olpe_model_kernel  build_analytical_model for one vector (test hook)
-//   olpe_chi2_kernel   chi_squared for a batch of vectors (the minimum slice)
+//   olpe_gibbs_kernel  fused sampler: W walkers, one per wavefront at a time (a
+//                      persistent grid whose waves take walkers from a device queue),
+//                      n_iters Gibbs iterations each (apf_step2.py:300-351) with the
+//                      cutout and inverse-sigma map staged once per workgroup into LDS
+//                      (64x64 and smaller; L2-resident above).
+//   olpe_eval_kernel   build_analytical_model / chi_squared of explicit parameter
+//                      vectors (olpe_model test hook, olpe_chi2_batch)
 //   olpe_seed_kernel   np.random.seed per walker
 //   olpe_stream_kernel RNG stream dump (test hook)
 #include <hip/hip_runtime.h>
