@@ -201,14 +201,22 @@ def main():
 
     # end-of-run exchange: RCCL all-gather of final walker states
     gather_ms = None
+    gather_err = None
     if world > 1 and not args.share_gpu:
-        uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
-        s.comm_init(uid, world, rank)
-        barrier()
-        tg = time.perf_counter()
-        allst = s.allgather_state()
-        gather_ms = allmax(time.perf_counter() - tg) * 1e3
-        assert allst.shape == (world * wpg, s.ps)
+        # outside the timed region; an error here (reported by libolpe) is recorded in
+        # the JSON line instead of losing the measurement
+        try:
+            uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
+            s.comm_init(uid, world, rank)
+            barrier()
+            tg = time.perf_counter()
+            allst = s.allgather_state()
+            gather_ms = allmax(time.perf_counter() - tg) * 1e3
+            if allst.shape != (world * wpg, s.ps):
+                raise RuntimeError(f"all-gather returned {allst.shape}")
+        except Exception as e:          # noqa: BLE001 -- reported, not hidden
+            gather_err = f"{type(e).__name__}: {e}"
+            print(f"[bench rank {rank}] all-gather failed: {gather_err}", file=sys.stderr)
 
     if rank != 0:
         s.close()
@@ -281,6 +289,8 @@ def main():
         "roofline": roofline(args.mode, kernel_ms),
         "allgather_ms": gather_ms,
     }
+    if gather_err:
+        out["allgather_error"] = gather_err
     if alt:
         other, alt_steps, e2, k2 = alt
         out["alt_eval"] = {"eval": other,
