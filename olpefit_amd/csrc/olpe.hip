@@ -129,6 +129,9 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
   s[0] = k.a; s[1] = k.b; s[2] = k.c;
 }
 
+#ifndef OLPE_CTRL_PRIO
+#define OLPE_CTRL_PRIO 1   // wave priority of the step's control chain (the sweep runs at 0)
+#endif
 #ifndef OLPE_GLOBAL_WAVES_PER_EU
 #define OLPE_GLOBAL_WAVES_PER_EU 3
 #endif
@@ -249,7 +252,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     ccache.colc = colc;
 #pragma unroll
     for (int g = 0; g < 2 * NSRC; ++g) ccache.E[g] = ccache.R[g] = 0.0;
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
 #ifdef OLPE_DIAG_TIMING
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long dt_last = __builtin_amdgcn_s_memtime();
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       const unsigned gmask = gauss_mask<NSRC>(r);
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask);
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
       DT_MARK(3);
       const double chi = wave_sum(part);
       DT_MARK(4);
