@@ -446,3 +446,51 @@ def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core):
         ref, rtr = ora.Walker(dm, err, p0, sd).run(400, trace=True)
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
         assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
+
+
+def test_one_shot_run_gibbs_c_abi(golden, lib_loaded):
+    """olpe_run_gibbs (SURVEY.md §8(b)'s one-shot entry point, host buffers in and out)
+    called through ctypes as INTEGRATION.md binds it: state, counters and chain equal
+    the oracle's run of the same seeds (burn-in 40, every iteration recorded)."""
+    import ctypes as C
+    g = golden("c32")
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    s = make_sampler(g)
+    W, n_it, burn = 3, 250, 40
+    seeds = np.array([5, 6, 7], np.uint32)
+    s.seed(seeds)
+    state = np.ascontiguousarray(np.tile(g["p_init"], (W, 1)))
+    tries = np.zeros((W, 16))
+    accepts = np.zeros((W, 16))
+    nrec = n_it - burn + 1
+    chain = np.empty((W, nrec, 17))
+    pd = C.POINTER(C.c_double)
+    rc = lib_loaded.olpe_run_gibbs(s._ctx, state.ctypes.data_as(pd), tries.ctypes.data_as(pd),
+                                   accepts.ctypes.data_as(pd), W, n_it, burn, 1,
+                                   chain.ctypes.data_as(pd))
+    assert rc == 0, lib_loaded.olpe_last_error()
+    for w, sd in enumerate(seeds):
+        walker = ora.Walker(dm, err, g["p_init"], int(sd))
+        ref, _ = walker.run(n_it, burn_in=burn)
+        np.testing.assert_allclose(chain[w], ref, rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(state[w], ref[-1], rtol=1e-9)
+    assert np.all(tries.sum(axis=1) == n_it) and np.all(accepts <= tries)
+
+
+def test_fixed_background_trajectories_match_oracle(golden, lib_loaded):
+    """bkgd_mode=1 (background = p[9], apf_step2.py:126-132, the build's --fixed-bkgd):
+    2 walkers x 500 iterations of the sampler against the oracle in the same mode."""
+    g = golden("c64")
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    p0 = g["p_init"].copy()
+    with np.errstate(all="ignore"):
+        p0[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p0, 64, 2, bkgd_mode=1),
+                                       err))
+    for mode in MODES:
+        s = make_sampler(g, mode, bkgd_mode=1)
+        s.seed([17, 18])
+        s.set_state(np.tile(p0, (2, 1)))
+        chain = s.run(500, burn_in=0, record_stride=1)
+        for w, sd in enumerate([17, 18]):
+            ref, _ = ora.Walker(dm, err, p0, sd, bkgd_mode=1).run(500)
+            np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
