@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "../../include/olpe.h"
@@ -606,11 +607,14 @@ template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   const size_t shm = lds_bytes(c, WPB);
   auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB, FAST>;
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the dynamic-LDS limit is a per-device function attribute: set once per device
+  // (contexts on several GPUs may launch from different host threads)
+  static std::atomic<uint64_t> attr_set{0};
+  const uint64_t bit = 1ull << (c->device & 63);
+  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
     HIPCHK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                160 * 1024));
-    attr_set = true;
+    attr_set.fetch_or(bit, std::memory_order_release);
   }
   unsigned blocks = (unsigned)((a.W + WPB - 1) / WPB);
   GibbsArgs q = a;
