@@ -119,6 +119,13 @@ __host__ __device__ constexpr int drawtab_extra(int nt) {
 }
 // bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
 __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
+// per-wave table area of the sampler: the V table (or the two FAST3 shape-table slots,
+// 2 x rows x 16 B, which fit in it); the 3-source 64x64 sampler keeps only the shape
+// tables (its V-table fallback runs the exact sweep instead) so that its LDS layout
+// fits 12 waves beside the cutout
+__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt) {
+  return (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
+}
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
   double *etab = reinterpret_cast<double *>(smem);
   double2 *sDE = reinterpret_cast<double2 *>(smem + kEtabBytes);
   constexpr int TABX = drawtab_extra(NT);
-  const int wstride = WS::BYTES + TABX + vtab_bytes(n, NSRC);
+  const int wstride = WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (size_t)wave * wstride;
   uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
@@ -594,7 +601,7 @@ template <class T> int dev_alloc(T **p, size_t count) {
 size_t wave_lds(int n, int np, bool lds_img) {
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
   return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
-         vtab_bytes(n, np == 16 ? 2 : 3);
+         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt);
 }
 
 size_t lds_bytes(const olpe_ctx *c, int wpb) {

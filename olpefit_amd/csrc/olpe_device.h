@@ -1132,7 +1132,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // LEAN: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): two-row
     // update and no shape-table prefetch; with 12 waves (WIDE, 168 VGPRs) and
     // elsewhere the four-row update with the prefetch
-    constexpr bool LEAN = NSRC == 2 && NT == 64 && !WIDE;
+    constexpr bool LEAN = (NSRC == 2 && NT == 64 && !WIDE) || (NSRC == 3 && NT == 64);
 #ifdef OLPE_ROWU
     constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
 #else
@@ -1365,7 +1365,8 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     // of keeping the guard's loads live (and spilled) across the row loop
     asm volatile("" ::: "memory");
     if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
-    if (lvl == 1) {
+    // (the 3-source 64x64 sampler has no room for the V table: sampler_vtab_bytes)
+    if (lvl == 1 && !(NSRC == 3 && NT == 64)) {
       if (hc) hc->valid = false;                           // the V table overwrites vtab
       return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
     }
