@@ -258,8 +258,6 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
     ccache.colc = colc;
-#pragma unroll
-    for (int g = 0; g < 2 * NSRC; ++g) ccache.E[g] = ccache.R[g] = 0.0;
     __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
 #ifdef OLPE_DIAG_TIMING
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
