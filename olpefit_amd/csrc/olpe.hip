@@ -646,7 +646,9 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
 template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &a) {
   if (c->lds_img) {
     switch (c->n) {
-      case 32: return launch_gibbs_t<NSRC, 32, true, 16, FAST>(c, a);
+      // 12 waves at 32x32 as well (168 VGPRs: no spills; 3-source +77 %, 2-source +1 %
+      // over 16)
+      case 32: return launch_gibbs_t<NSRC, 32, true, 12, FAST>(c, a);
       case 64: {
         // 12 waves per workgroup (168 VGPRs: four-row update and shape-table prefetch
         // without spills, 3 waves per SIMD with the walker queue keeping them busy):
@@ -741,8 +743,8 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   c->ps = c->np + 1;
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside a workgroup's wave slices (12 waves
-  // at 64x64, 16 otherwise; launch_gibbs_m)
-  c->lds_img = npix * sizeof(double2) + (nx == 64 ? 12 : 16) * wave_lds(nx, c->np, true) +
+  // at 32x32 and 64x64, 16 for other sides; launch_gibbs_m)
+  c->lds_img = npix * sizeof(double2) + ((nx == 64 || nx == 32) ? 12 : 16) * wave_lds(nx, c->np, true) +
                    kEtabBytes <= 160 * 1024;
   if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
 
