@@ -1132,7 +1132,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // LEAN: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): two-row
     // update and no shape-table prefetch; with 12 waves (WIDE, 168 VGPRs) and
     // elsewhere the four-row update with the prefetch
-    constexpr bool LEAN = (NSRC == 2 && NT == 64 && !WIDE) || (NSRC == 3 && NT == 64);
+    constexpr bool LEAN = (NSRC == 2 && NT == 64 && !WIDE) || (NSRC == 3 && (NT == 64 || NT == 32));
 #ifdef OLPE_ROWU
     constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
 #else

@@ -391,12 +391,13 @@ def test_walker_queue_equals_static_mapping(golden, lib_loaded, monkeypatch):
 
 @pytest.mark.parametrize("n,nsrc,mode", [(40, 2, "fast"), (40, 2, "exact"), (48, 3, "fast"),
                                          (80, 2, "fast"), (96, 3, "fast"), (128, 2, "fast"),
-                                         (24, 2, "fast")])
+                                         (24, 2, "fast"), (32, 3, "fast"), (32, 3, "exact"),
+                                         (64, 3, "fast")])
 def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
     """Cutout sides without a dedicated kernel (runtime-n LDS sampler for n <= ~72,
     global-memory sampler above; 128 with two sources; n < 32 with several row groups
-    per wave, n not dividing 64): model, chi^2 and 3 walkers x 300 iterations against
-    the oracle on the synthetic frame of that size."""
+    per wave, n not dividing 64) and the 3-source 32x32 / 64x64 kernels on synthetic
+    frames: model, chi^2 and 3 walkers x 300 iterations against the oracle."""
     from olpefit_amd import synth
     from olpefit_amd.core import Sampler
     from olpefit_amd.pipeline import initial_parameters
