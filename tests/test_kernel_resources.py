@@ -1,0 +1,64 @@
+"""Register / scratch budget of the bench sampler kernels (CPU: a device-only hipcc
+compile with the resource-usage remarks, no GPU).
+
+The 64x64 two-source sampler runs 12 waves per workgroup (3 per SIMD), which caps a
+wave at 168 VGPRs; DESIGN.md §3 relies on it having no scratch at all (spilled column
+terms cost the 16-wave variant 0.25 GB of extra HBM writes per launch).  A change that
+makes the FAST or EXACT bench kernel spill fails here before it reaches a GPU.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+@pytest.fixture(scope="module")
+def usage():
+    if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
+        pytest.skip("hipcc not available")
+    from olpefit_amd import build
+    flags = [f for f in build.FLAGS if f not in ("-shared", "-fPIC", "-Wall",
+                                                  "-Wno-unused-function")]
+    cmd = [HIPCC, *flags, "--cuda-device-only", "-c", "-o", os.devnull,
+           os.path.join(REPO, "olpefit_amd", "csrc", "olpe.hip"),
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900).stderr
+    res = {}
+    name = None
+    for line in out.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            res[name] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs|ScratchSize \[bytes/lane\]|VGPRs Spill): (\d+)", line)
+        if m and name:
+            res[name][m.group(1)] = int(m.group(2))
+    return res
+
+
+def _kernel(usage, nsrc, nt, lds, wpb, fast):
+    key = (f"olpe_gibbs_kernelILi{nsrc}ELi{nt}ELb{int(lds)}ELi{wpb}ELb{int(fast)}E")
+    hits = [v for k, v in usage.items() if key in k]
+    assert hits, f"kernel {key} not found in the resource remarks"
+    return hits[0]
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_bench_sampler_has_no_scratch(usage, fast):
+    k = _kernel(usage, 2, 64, True, 12, fast)
+    assert k["ScratchSize [bytes/lane]"] == 0, k
+    assert k["VGPRs"] <= 168, k
+
+
+def test_other_bench_configs_have_no_scratch(usage):
+    # configs[4] (3-source 128x128, global-memory sampler, 3 workgroups of 4 waves)
+    # and the 3-source 64x64 LDS sampler
+    for args in [(3, 128, False, 4, True), (3, 64, True, 12, True)]:
+        k = _kernel(usage, *args)
+        assert k["ScratchSize [bytes/lane]"] == 0, (args, k)
