@@ -146,7 +146,8 @@ def main():
     ap.add_argument("--mode", default="fast", choices=["exact", "fast"])
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the single-GPU measurement of the other eval mode")
-    ap.add_argument("--cpu-iters", type=int, default=2000)
+    ap.add_argument("--cpu-iters", type=int, default=6000,
+                    help="oracle iterations per CPU process (about 10-30 s of CPU work in total)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-gpu", action="store_true",
