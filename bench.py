@@ -146,8 +146,9 @@ def main():
     ap.add_argument("--mode", default="fast", choices=["exact", "fast"])
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the single-GPU measurement of the other eval mode")
-    ap.add_argument("--cpu-iters", type=int, default=6000,
-                    help="oracle iterations per CPU process (about 10-30 s of CPU work in total)")
+    ap.add_argument("--cpu-iters", type=int, default=None,
+                    help="oracle iterations per CPU process (default: about 12-20 s of CPU "
+                         "work in total: 6000 at 64x64, 6000*64^2/n^2 otherwise, at least 500)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--share-gpu", action="store_true",
@@ -300,7 +301,8 @@ def main():
                            "roofline": roofline(other, k2)}
     if not args.no_cpu_baseline and world == 1:
         procs = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(n, nsrc, args.cpu_iters, procs)
+        cpu_iters = args.cpu_iters or max(500, 6000 * 64 * 64 // (n * n))
+        out["cpu_baseline"] = cpu_baseline(n, nsrc, cpu_iters, procs)
     print(json.dumps(out))
     s.close()
     group.close()
