@@ -495,3 +495,32 @@ def test_fixed_background_trajectories_match_oracle(golden, lib_loaded):
         for w, sd in enumerate([17, 18]):
             ref, _ = ora.Walker(dm, err, p0, sd, bkgd_mode=1).run(500)
             np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_degenerate_runs(golden, lib_loaded, mode):
+    """Edge cases of the loop bookkeeping (apf_step2.py:300-351): an empty ensemble is
+    refused, a zero-iteration launch changes nothing, a launch that ends inside the
+    burn-in records no rows, and a single walker / a walker count that fills no
+    workgroup evenly (13) follow the oracle."""
+    from olpefit_amd.core import OlpeError
+    g = golden("c64")
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    s = make_sampler(g, mode)
+    with pytest.raises(OlpeError):
+        s.seed([])
+    for seeds in ([7], list(range(40, 53))):
+        s.seed(seeds)
+        s.set_state(np.tile(g["p_init"], (len(seeds), 1)))
+        before = s.get_state()
+        assert s.run(0, burn_in=0, record_stride=1) is None
+        for x, y in zip(before, s.get_state()):
+            np.testing.assert_array_equal(x, y)
+        assert s.count == 0
+        assert s.run(50, burn_in=80, record_stride=1) is None      # inside the burn-in
+        chain = s.run(70, burn_in=80, record_stride=3)             # rows at 80, 83, ..., 119
+        assert chain.shape == (len(seeds), 14, 17) and s.count == 120
+        for w in (0, len(seeds) - 1):
+            ref, _ = ora.Walker(dm, err, g["p_init"], seeds[w]).run(120, burn_in=80,
+                                                                     record_stride=3)
+            np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
