@@ -37,7 +37,13 @@ def load_chains(input_directory: str, ncor: int, additional_burnin: int = 1):
 
 
 def gelman_rubin(p, d: int = 16):
-    """apf_step3.py:260-276 for one parameter: p [N, M] (rows, walkers) -> (PSRF, RC)."""
+    """apf_step3.py:260-276 (3body/apf_step3_3body.py:294-310) for one parameter:
+    p [N, M] (rows, walkers) -> (PSRF, RC).
+
+    The reference is Python 2 without ``from __future__ import division``, so its
+    ``RC = np.sqrt(((d+3)/(d+1))*PSRF)`` with the int ``d = 16`` (:264, :276) divides
+    19 by 17 as integers: the factor is 1 and RC = sqrt(PSRF).  Integer ``d`` keeps
+    that floor division here; a float ``d`` divides as floats, as it would there."""
     p = np.asarray(p, dtype=np.float64)
     N, M = float(p.shape[0]), float(p.shape[1])
     ncor = p.shape[1]
@@ -51,16 +57,19 @@ def gelman_rubin(p, d: int = 16):
     b = (N / (M - 1)) * np.sum(b)
     pooled = ((N - 1) / N) * w + ((M + 1) / (M * N)) * b
     psrf = pooled / w
-    return psrf, np.sqrt(((d + 3) / (d + 1)) * psrf)
+    factor = (d + 3) // (d + 1) if isinstance(d, (int, np.integer)) else (d + 3) / (d + 1)
+    return psrf, np.sqrt(factor * psrf)
 
 
 def summary(chains, nsrc: int = 2):
-    """Per-parameter mean, median, std and Gelman-Rubin RC over [N, M, PS] chains."""
+    """Per-parameter mean, median, std and Gelman-Rubin PSRF / RC over [N, M, PS]
+    chains (the chi^2 column is not a GR parameter: apf_step3.py:260,
+    3body/apf_step3_3body.py:294)."""
     names = NAMES_2 if nsrc == 2 else NAMES_3
     out = {}
     for k, name in enumerate(names[:-1]):
         x = chains[:, :, k]
-        _, rc = gelman_rubin(x)
+        psrf, rc = gelman_rubin(x)
         out[name] = {"mean": float(np.mean(x)), "median": float(np.median(x)),
-                     "std": float(np.std(x)), "gr_rc": float(rc)}
+                     "std": float(np.std(x)), "gr_psrf": float(psrf), "gr_rc": float(rc)}
     return out

@@ -316,8 +316,11 @@ def run_walkers(image_nanmask, err, p0, seeds, n_iters, nsrc=2, bkgd_mode=0, bur
 # ----------------------------------------------------------------------------------
 
 def gelman_rubin(chains, d=16):
-    """apf_step3.py:260-278.  ``chains``: array [length, ncor] for one parameter.
-    Returns (PSRF, RC)."""
+    """apf_step3.py:260-278 (3body/apf_step3_3body.py:294-310).  ``chains``: array
+    [length, ncor] for one parameter.  Returns (PSRF, RC).
+
+    Python-2 semantics: the reference's ``(d+3)/(d+1)`` with int d = 16 is integer
+    division (== 1), so RC = sqrt(PSRF)."""
     p = np.asarray(chains, dtype=np.float64)
     N, M = float(p.shape[0]), float(p.shape[1])
     ncor = p.shape[1]
@@ -331,5 +334,5 @@ def gelman_rubin(chains, d=16):
     b = (N / (M - 1)) * np.sum(b)
     pooled_variance = ((N - 1) / N) * w + ((M + 1) / (M * N)) * b
     psrf = pooled_variance / w
-    rc = np.sqrt(((d + 3) / (d + 1)) * psrf)
+    rc = np.sqrt(((d + 3) // (d + 1)) * psrf)       # Python 2 int division: 19 / 17 == 1
     return psrf, rc

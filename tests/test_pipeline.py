@@ -105,26 +105,42 @@ def test_noise_model_matches_oracle(golden):
 def test_step3_reader_and_gelman_rubin(tmp_path, golden):
     """Write chains with the build's writer, read them back with the step-3 contract
     (equal lengths, NaN row dropped by additional_burnin=1) and compare GR with the
-    oracle's restatement of apf_step3.py:260-278."""
-    rs = np.random.RandomState(3)
-    chains = rs.normal(size=(4, 50, 17))
-    for w in range(4):
-        pipeline.write_chain_csv(str(tmp_path / f"{w}_finalarray_mpi.csv"),
-                                 pipeline.with_seed_row(chains[w]))
-    c = step3.load_chains(str(tmp_path), 4, additional_burnin=1)
-    assert c.shape == (50, 4, 17)
-    assert np.array_equal(c[:, 2, :], chains[2])
-    for k in range(16):
-        ps1, rc1 = step3.gelman_rubin(c[:, :, k])
-        ps2, rc2 = ora.gelman_rubin(c[:, :, k])
-        assert ps1 == ps2 and rc1 == rc2
-    s = step3.summary(c)
-    assert set(s) == set(step3.NAMES_2[:-1])
+    hand-pinned fixture (tests/golden/make_gr_golden.py: exact rational arithmetic,
+    Python-2 integer (d+3)/(d+1) == 1) for 17- and 20-column chains.  Tolerance rel
+    1e-9: float64 cancellation in the variances against the exact values; the
+    Python-3 factor sqrt(19/17) would be off by 5.7e-2."""
+    g = golden("gr")
+    for tag, nsrc, names in (("2", 2, step3.NAMES_2), ("3", 3, step3.NAMES_3)):
+        chains = g[f"chains{tag}"]                    # [N, M, PS]
+        N, M, ps = chains.shape
+        d = tmp_path / tag
+        d.mkdir()
+        for w in range(M):
+            pipeline.write_chain_csv(str(d / f"{w}_finalarray_mpi.csv"),
+                                     pipeline.with_seed_row(chains[:, w, :]))
+        c = step3.load_chains(str(d), M, additional_burnin=1)
+        assert c.shape == (N, M, ps)
+        assert np.array_equal(c, chains)              # repr round trip is exact
+        for k in range(ps - 1):
+            ps1, rc1 = step3.gelman_rubin(c[:, :, k])
+            np.testing.assert_allclose(ps1, g[f"psrf{tag}"][k], rtol=1e-9)
+            np.testing.assert_allclose(rc1, g[f"rc{tag}"][k], rtol=1e-9)
+            assert rc1 == np.sqrt(ps1)                # factor (16+3)//(16+1) == 1
+            ps2, rc2 = ora.gelman_rubin(c[:, :, k])
+            assert ps1 == ps2 and rc1 == rc2
+        s = step3.summary(c, nsrc=nsrc)
+        assert list(s) == names[:-1]
+        np.testing.assert_allclose([s[n]["gr_rc"] for n in names[:-1]], g[f"rc{tag}"],
+                                   rtol=1e-9)
+    # a float d divides as floats, as it would in the reference with d = 16.
+    x = g["chains2"][:, :, 0]
+    assert step3.gelman_rubin(x, d=16.0)[1] == np.sqrt((19 / 17) * step3.gelman_rubin(x)[0])
     # unequal lengths are an error, as in the reference's [length, ncor] assignment
-    pipeline.write_chain_csv(str(tmp_path / "3_finalarray_mpi.csv"),
-                             pipeline.with_seed_row(chains[3][:10]))
+    chains = g["chains2"]
+    pipeline.write_chain_csv(str(tmp_path / "2" / "3_finalarray_mpi.csv"),
+                             pipeline.with_seed_row(chains[:10, 3, :]))
     with pytest.raises(ValueError):
-        step3.load_chains(str(tmp_path), 4)
+        step3.load_chains(str(tmp_path / "2"), 5)
 
 
 def test_headless_step1_guess(tmp_path):
