@@ -12,8 +12,18 @@ Workload (BASELINE.json configs[2]): 65,536 walkers p
 GPU on a synthetic 64x64 two-source NIRC2 cutout, fp64, chain stride 10.  For N > 1
 GPUs the driver launches one process per GPU (torch.distributed.run); walkers are
 sharded with seeds 1000 + global walker index, there is no communication while
-sampling, and the end-of-run RCCL all-gather of final states (outside the timed
-region, reported as ``allgather_ms``) is the only exchange.  ``scaling`` is "weak".
+sampling, and the end-of-run RCCL exchange (outside the timed region) is the only
+one: all-gather of the final states (``allgather_ms``) and the chain concatenation
+(all-gather of the last launch's chain rows over xGMI, in walker ranges that bound the
+receive buffer: ``chain_gather_ms`` / ``_bytes`` / ``_gbs``).  ``scaling`` is "weak".
+The host group (barrier, max-over-ranks time, RCCL id) is stdlib TCP, no PyTorch.
+
+Roofline: the kernel is FP64-VALU bound.  ``roofline.frac`` = executed
+FP64 VALU lane-ops per second / 39.3e12 (78.6 TFLOP/s with FMA = 2), the executed
+count per walker-step read from the rocprofv3 SQ counters of this config
+(profiles/valu_counts.json, tools/pmc_valu.sh) times the live HIP-event rate;
+``valu_issue_frac`` does the same with all VALU instructions.  The HBM figures use the
+PMC FETCH/WRITE bytes per launch (profiles/pmc_traffic.json).
 
 Rank 0 prints ONE JSON line.
 """
@@ -46,14 +56,15 @@ CONFIG_NAMES = {
     4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
 }
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
-EXP_OPS = 20                      # FP64 VALU ops of one ocml exp(f64)
+HBM_PEAK = 8.0e12                 # MI355X HBM3E spec (MI355X_MICROARCH.md)
+EXP_OPS = 19                      # FP64 VALU ops of one ocml exp(f64), ISA count
 EXP_TAB_OPS = 12                  # FP64 VALU ops of olpe::exp_tab (FAST3 setup)
 
 
 def work_per_step(n: int, nsrc: int, mode: str) -> float:
     """FP64 VALU lane-ops of one walker-step's model + chi^2 evaluation.
 
-    exact: per pixel-Gaussian 7 ops + one exp (E = 20), per pixel G-1 combines +
+    exact: per pixel-Gaussian 7 ops + one exp (E = 19), per pixel G-1 combines +
            background + 3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel, with
            the four-row update, 2 sets x (5m-1)/4 (m = nsrc Gaussians per set; G
@@ -103,29 +114,54 @@ def _cpu_worker(args):
     return time.perf_counter() - t
 
 
-def cpu_baseline(n: int, nsrc: int, iters: int, procs: int):
+def host_cpus():
+    """(cores usable by this process, CPUs in its affinity mask, cgroup CPU quota or
+    None, model name).  On the GPU box the affinity mask shows the whole machine
+    while the job's cgroup quota grants a share of it; more processes than the
+    quota only time-slice."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, aff, quota, model or platform.processor()
+
+
+def cpu_baseline(n: int, nsrc: int, total_iters: int):
+    """The oracle (one walker per process, like one MPI rank per walker) on every core
+    this job may use, ``total_iters`` walker-steps in all (about 12 s of CPU work)."""
+    procs, aff, quota, model = host_cpus()
+    iters = max(200, total_iters // procs)
     with mp.get_context("spawn").Pool(procs) as pool:
         pool.map(_cpu_worker, [(n, nsrc, 1, 5)] * procs)          # import warm-up
         t0 = time.perf_counter()
         times = pool.map(_cpu_worker, [(n, nsrc, 1000 + i, iters) for i in range(procs)])
         wall = time.perf_counter() - t0
     steps = procs * iters
-    cpu_model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {"value": steps / wall, "unit": "walker-steps/s", "cores": procs, "kind": "port",
-            "sample": f"oracle/olpe_oracle.py NumPy restatement, {procs} processes x 1 walker "
-                      f"x {iters} iterations, {n}x{n} {nsrc}-source cutout "
-                      f"({sum(times):.1f} s CPU); cpu: {cpu_model or platform.processor()}"}
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_model": model,
+            "sample": f"oracle/olpe_oracle.py NumPy restatement, {procs} processes (one per "
+                      f"usable core: affinity {aff} CPUs, cgroup quota "
+                      f"{'none' if quota is None else f'{quota:g}'}) x 1 walker x {iters} "
+                      f"iterations, {n}x{n} {nsrc}-source cutout ({sum(times):.1f} s CPU); "
+                      f"cpu: {model}"}
 
 
-def load_traffic(path: str):
+def load_json(path: str):
     try:
         with open(path) as f:
             return json.load(f)
@@ -146,11 +182,15 @@ def main():
     ap.add_argument("--mode", default="fast", choices=["exact", "fast"])
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the single-GPU measurement of the other eval mode")
-    ap.add_argument("--cpu-iters", type=int, default=None,
-                    help="oracle iterations per CPU process (default: about 12-20 s of CPU "
-                         "work in total: 6000 at 64x64, 6000*64^2/n^2 otherwise, at least 500)")
+    ap.add_argument("--cpu-steps", type=int, default=None,
+                    help="oracle walker-steps in all, spread over one process per usable "
+                         "core (default: about 12 s of CPU work: 96,000 at 64x64, scaled by "
+                         "64^2/n^2 otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--valu", default=os.path.join(REPO, "profiles", "valu_counts.json"))
+    ap.add_argument("--gather-mib", type=float, default=1024.0,
+                    help="N > 1: MiB of chain rows per rank per all-gather range")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0, no RCCL "
                          "all-gather (RCCL refuses two ranks on one device)")
@@ -177,6 +217,8 @@ def main():
     s.set_state(np.tile(p0, (wpg, 1)))
 
     def measure(mode, steps, warmup):
+        # launches are queued back to back (no host sync between them) and their
+        # HIP-event durations read afterwards (olpe_kernel_times)
         s.set_eval_mode(mode)
         for _ in range(warmup):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
@@ -185,15 +227,20 @@ def main():
         s.sync()
         t0 = time.perf_counter()
         kms = []
-        for _ in range(steps):
+        for i in range(steps):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
-            kms.append(s.last_kernel_ms())      # HIP events on the launch stream
+            if (i + 1) % 64 == 0:                # the event ring holds 64 launches
+                kms.extend(s.kernel_times(64))
         s.sync()
         barrier()
         t1 = time.perf_counter()
+        if steps % 64:
+            kms.extend(s.kernel_times(steps % 64))
         return allmax(t1 - t0), float(np.mean(kms))
 
     elapsed, kernel_ms = measure(args.mode, args.steps, args.warmup)
+    st, tries, accs = s.get_state()
+    acceptance = float(accs.sum() / max(1.0, tries.sum()))
     alt = None
     if world == 1 and not args.no_alt:
         other = "exact" if args.mode == "fast" else "fast"
@@ -201,24 +248,38 @@ def main():
         e2, k2 = measure(other, alt_steps, 1)
         alt = (other, alt_steps, e2, k2)
 
-    # end-of-run exchange: RCCL all-gather of final walker states
-    gather_ms = None
-    gather_err = None
+    # end-of-run exchange over RCCL/xGMI, outside the timed region:
+    # all-gather of the final walker states, then the chain concatenation -- the last
+    # launch's chain rows of every rank, gathered range by range so that the receive
+    # buffer stays under --gather-mib per rank.  An error (reported by libolpe) is
+    # recorded in the JSON line instead of losing the measurement.
+    comm = {}
     if world > 1 and not args.share_gpu:
-        # outside the timed region; an error here (reported by libolpe) is recorded in
-        # the JSON line instead of losing the measurement
         try:
             uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
             s.comm_init(uid, world, rank)
             barrier()
             tg = time.perf_counter()
             allst = s.allgather_state()
-            gather_ms = allmax(time.perf_counter() - tg) * 1e3
+            comm["allgather_ms"] = allmax(time.perf_counter() - tg) * 1e3
             if allst.shape != (world * wpg, s.ps):
                 raise RuntimeError(f"all-gather returned {allst.shape}")
+            per_walker = s._nrec * s.ps * 8
+            wn = max(1, min(wpg, int(args.gather_mib * 2 ** 20 // max(1, per_walker))))
+            s.allgather_chain(0, min(wn, wpg), out=False)         # warm-up (buffer, rings)
+            barrier()
+            tc = time.perf_counter()
+            for w0 in range(0, wpg, wn):
+                s.allgather_chain(w0, min(wn, wpg - w0), out=False)
+            t = allmax(time.perf_counter() - tc)
+            nbytes = world * wpg * per_walker
+            comm.update(chain_gather_ms=t * 1e3, chain_gather_bytes=nbytes,
+                        chain_gather_ranges=(wpg + wn - 1) // wn,
+                        chain_gather_gbs=nbytes * (world - 1) / world / t / 1e9)
         except Exception as e:          # noqa: BLE001 -- reported, not hidden
-            gather_err = f"{type(e).__name__}: {e}"
-            print(f"[bench rank {rank}] all-gather failed: {gather_err}", file=sys.stderr)
+            comm["comm_error"] = f"{type(e).__name__}: {e}"
+            print(f"[bench rank {rank}] RCCL exchange failed: {comm['comm_error']}",
+                  file=sys.stderr)
 
     if rank != 0:
         s.close()
@@ -228,48 +289,61 @@ def main():
     total = world * wpg * args.iters * args.steps
     value = total / elapsed
     steps_per_launch = wpg * args.iters
-    traffic = load_traffic(args.traffic)
+    traffic = load_json(args.traffic) or {}
+    valu = load_json(args.valu) or {}
+    from olpefit_amd.build import kernel_digest
+    digest = kernel_digest()
+    default_shape = not args.walkers and args.iters == 100 and args.stride == 10
 
-    def traffic_of(mode):
-        # PMC bytes per launch, measured for this config at the default launch shape
-        # (walkers, iterations, stride); null for any other workload
-        if args.walkers or args.iters != 100 or args.stride != 10:
-            return None
-        key = mode if args.config == 2 else f"c{args.config}_{mode}"
-        return (traffic or {}).get(key, {}).get("bytes_per_launch")
+    def key(mode):
+        return mode if args.config == 2 else f"c{args.config}_{mode}"
 
     def roofline(mode, kernel_ms):
-        # achieved = SURVEY.md §8(d)'s algorithmic work per walker-step (the exp-form
-        # count, E = 20) x walker-steps per launch / HIP-event kernel time.  The FAST
-        # algorithm does fewer operations than that count (no per-pixel exp), so its
-        # frac can exceed 1; executed_* is the operation count the kernel really issues
-        # (work_per_step) and measures how well the FP64 VALU is used.
-        algo = sec8d_work(n, nsrc)
+        """FP64-VALU roofline of the sampler kernel.  frac: executed
+        FP64 lane-ops (rocprofv3 SQ counts per walker-step, profiles/valu_counts.json)
+        x the live HIP-event walker-step rate / the FP64 vector peak."""
         secs = kernel_ms * 1e-3
-        achieved = steps_per_launch * algo / secs / 1e12
-        ops = work_per_step(n, nsrc, mode)
-        executed = steps_per_launch * ops / secs / 1e12
+        rate = steps_per_launch / secs                   # walker-steps/s of the kernel
         peak = FP64_LANE_PEAK / 1e12
-        return {
-            "bound": "fp64-valu",
-            "achieved": achieved,
-            "peak": peak,
-            "unit": "TFLOP/s",
-            "frac": achieved / peak,
-            "traffic": traffic_of(mode),
-            "kernel": "olpe_gibbs_kernel",
-            "kernel_ms": kernel_ms,
-            "algorithmic_work_per_walker_step": algo,
-            "walker_steps_per_launch": steps_per_launch,
-            "executed_work_per_walker_step": ops,
-            "executed_achieved": executed,
-            "executed_frac": executed / peak,
-            "note": "FP64 VALU lane-ops (FMA counted once; SURVEY.md 8(d)) per second, peak "
-                    "= 78.6 TFLOP/s / 2; achieved uses the 8(d) exp-form work Np(12G+8) + "
-                    "E Np G, executed_* the kernel's own operation count (DESIGN.md §4); "
-                    "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
-                    "(profiles/pmc_traffic.json)",
-        }
+        vc = valu.get(key(mode))       # per walker-step, measured at the default shape
+        out = {"bound": "fp64-valu", "peak": peak, "unit": "TFLOP/s",
+               "kernel": "olpe_gibbs_kernel", "kernel_ms": kernel_ms,
+               "walker_steps_per_launch": steps_per_launch}
+        if vc:
+            out.update(
+                achieved=rate * vc["fp64_lane_ops_per_step"] / 1e12,
+                frac=rate * vc["fp64_lane_ops_per_step"] / FP64_LANE_PEAK,
+                frac_source="counters",
+                fp64_lane_ops_per_walker_step=vc["fp64_lane_ops_per_step"],
+                valu_per_walker_step=vc["valu_per_step"],
+                valu_issue_frac=rate * vc["valu_per_step"] * 64 / FP64_LANE_PEAK,
+                counts_stale=vc.get("kernel_digest") != digest)
+        else:                       # no counters for this shape: the model's own count
+            ops = work_per_step(n, nsrc, mode)
+            out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
+                       frac_source="operation count (model + chi^2 only; lower bound)",
+                       fp64_lane_ops_per_walker_step=ops)
+        ops = work_per_step(n, nsrc, mode)
+        out["model_chi2_frac"] = rate * ops / FP64_LANE_PEAK
+        algo = sec8d_work(n, nsrc)
+        out["equivalent_exp_form_rate"] = rate * algo / 1e12
+        out["exp_form_work_per_walker_step"] = algo
+        tb = traffic.get(key(mode), {}).get("bytes_per_launch") if default_shape else None
+        out["traffic"] = tb
+        out["hbm_gbs"] = tb / secs / 1e9 if tb else None
+        out["hbm_frac"] = tb / secs / HBM_PEAK if tb else None
+        out["note"] = (
+            "frac = executed FP64 VALU lane-ops (64 x SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 "
+            "per walker-step, FMA counted once) x HIP-event rate / 78.6e12/2; "
+            "valu_issue_frac = all VALU instructions x 64 / the same peak; model_chi2_frac = "
+            "the model + chi^2 operations alone (DESIGN.md §4); equivalent_exp_form_rate = "
+            "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 19) at this rate, in T "
+            "lane-ops/s: FAST does far fewer operations, so it is no utilisation figure; "
+            "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
+            "(profiles/pmc_traffic.json); the north star's >= 40 % HBM-read roofline does "
+            "not apply to an LDS-resident FP64-VALU-bound kernel (SURVEY.md 8(d)): hbm_frac "
+            "is reported, not targeted")
+        return out
 
     out = {
         "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
@@ -289,10 +363,10 @@ def main():
                    "chain_stride": args.stride, "eval": args.mode,
                    "parallelism": f"walker-sharded x{world}"},
         "roofline": roofline(args.mode, kernel_ms),
-        "allgather_ms": gather_ms,
+        "acceptance": acceptance,
+        "allgather_ms": None,
     }
-    if gather_err:
-        out["allgather_error"] = gather_err
+    out.update(comm)
     if alt:
         other, alt_steps, e2, k2 = alt
         out["alt_eval"] = {"eval": other,
@@ -300,9 +374,9 @@ def main():
                            "ms_per_step": e2 / alt_steps * 1e3,
                            "roofline": roofline(other, k2)}
     if not args.no_cpu_baseline and world == 1:
-        procs = min(16, os.cpu_count() or 1)
-        cpu_iters = args.cpu_iters or max(500, 6000 * 64 * 64 // (n * n))
-        out["cpu_baseline"] = cpu_baseline(n, nsrc, cpu_iters, procs)
+        cpu_steps = args.cpu_steps or max(4000, 96000 * 64 * 64 // (n * n))
+        out["cpu_baseline"] = cpu_baseline(n, nsrc, cpu_steps)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     print(json.dumps(out))
     s.close()
     group.close()

@@ -49,10 +49,15 @@ typedef struct olpe_ctx olpe_ctx;
 int olpe_version(void);
 /* Number of visible HIP devices (0 on a host without a GPU). */
 int olpe_device_count(int *count);
+/* Free / total device memory of a HIP device (sizes a run's launches so that the
+ * per-launch chain buffer fits; OLPE_EHIP without a GPU). */
+int olpe_device_mem(int device, long long *free_bytes, long long *total_bytes);
 /* Thread-local message describing the last error. */
 const char *olpe_last_error(void);
 
-/* Create a context for one N x N cutout.  Replaces the setup at apf_step2.py:160-237:
+/* Create a context for one N x N cutout.  Replaces the setup at apf_step2.py:160-237
+ * (the environment knob OLPE_WPB, a tuning experiment, must be 8, 12 or 16 and fit the
+ * LDS, else OLPE_EINVAL with the byte count):
  *   image      ny*nx row-major, float32 (image_dtype OLPE_DTYPE_F32, BITPIX -32) or
  *              float64; promoted to f64 exactly as ``data - model`` does (:135).
  *   pois2      |D| Poisson term squared, same dtype as image, rounded as the
@@ -136,6 +141,9 @@ int olpe_trace_read(olpe_ctx *ctx, double *out);
 int olpe_sync(olpe_ctx *ctx);
 /* Duration (ms, HIP events on the launch stream) of the last sampler launch. */
 int olpe_last_kernel_ms(olpe_ctx *ctx, double *ms);
+/* Durations of the last n sampler launches (oldest first; n <= 64 and <= launches so
+ * far): launches can be queued back to back and timed afterwards. */
+int olpe_kernel_times(olpe_ctx *ctx, int n, double *ms_out);
 
 /* --- chain files (apf_step2.py:342-360; 3body/apf_step2_3body.py:381-399) ---------
  * Host-only (no GPU needed).  Rows are formatted as the reference's csv.writer writes
@@ -152,12 +160,35 @@ int olpe_csv_format(const double *rows, long long nrows, int ncols, int nan_row,
 int olpe_csv_write_chains(const char *const *paths, const double *chains, int nfiles,
                           long long nrows, int ncols, int nan_row, int threads);
 
+/* Streaming form of the same files.  The reference rewrites each file every 10
+ * iterations (apf_step2.py:355-360), so a killed run leaves its chains on disk; the
+ * build appends each launch's rows instead: rows [0, nrows) of
+ * chains[i][rows_per_file][ncols] are appended to file i (created if absent; no NaN
+ * row -- write it first with olpe_csv_write_chains and nrows 0).  sizes_out [nfiles]
+ * (may be NULL) receives each file's size in bytes after the append: a checkpoint
+ * records it, and a resumed run truncates the file back to it. */
+int olpe_csv_append_chains(const char *const *paths, const double *chains, int nfiles,
+                           long long rows_per_file, long long nrows, int ncols, int threads,
+                           long long *sizes_out);
+
 /* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
 int olpe_comm_unique_id(uint8_t *id128);
 int olpe_comm_init(olpe_ctx *ctx, const uint8_t *id128, int nranks, int rank);
-/* All-gather the walker states of every rank: out [nranks*W][PS] (rank-major). */
+/* All-gather the walker states of every rank: out [nranks*W][PS] (rank-major; equal W
+ * on every rank, checked). */
 int olpe_comm_allgather_state(olpe_ctx *ctx, double *out);
+/* Chain concatenation (north star: "RCCL all-gather over xGMI only for the final chain
+ * concatenation"; the reference leaves one {rank}_finalarray_mpi.csv per MPI rank,
+ * apf_step2.py:355-360): all-gather walkers [w0, w0+wn) of the last launch's chain
+ * from every rank into out [nranks][wn][nrec][PS] (rank-major; host memory, or NULL to
+ * leave the gathered range in the context's device buffer, e.g. to time the
+ * collective alone).  Gathering a large ensemble range by range bounds both the device
+ * receive buffer and the host buffer by the range.  *nrec_out (may be NULL) = nrec.
+ * Every rank must call with the same range and have the same W and nrec (checked:
+ * OLPE_EINVAL on every rank otherwise). */
+int olpe_comm_allgather_chain(olpe_ctx *ctx, long long w0, long long wn, double *out,
+                              long long *nrec_out);
 /* All-reduce per-parameter moments of the last launch's chain (or of the final
  * states when no chain was recorded): out[3*PS] = {n, sum[PS], sumsq[PS]} with n
  * repeated in slot 0 of the first block, see DESIGN.md §6. */

@@ -36,6 +36,7 @@ _pll = C.POINTER(C.c_longlong)
 SIGNATURES = {
     "olpe_version": (_i, []),
     "olpe_device_count": (_i, [C.POINTER(_i)]),
+    "olpe_device_mem": (_i, [_i, _pll, _pll]),
     "olpe_last_error": (C.c_char_p, []),
     "olpe_create": (_i, [_P, _i, _P, _d, _pu8, _i, _i, _i, _i, _i, C.POINTER(_P)]),
     "olpe_destroy": (None, [_P]),
@@ -58,12 +59,15 @@ SIGNATURES = {
     "olpe_trace_read": (_i, [_P, _pd]),
     "olpe_sync": (_i, [_P]),
     "olpe_last_kernel_ms": (_i, [_P, _pd]),
+    "olpe_kernel_times": (_i, [_P, _i, _pd]),
     "olpe_csv_format": (_i, [_pd, _ll, _i, _i, C.c_char_p, C.c_size_t,
                              C.POINTER(C.c_size_t)]),
     "olpe_csv_write_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _i, _i, _i]),
+    "olpe_csv_append_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _ll, _i, _i, _pll]),
     "olpe_comm_unique_id": (_i, [_pu8]),
     "olpe_comm_init": (_i, [_P, _pu8, _i, _i]),
     "olpe_comm_allgather_state": (_i, [_P, _pd]),
+    "olpe_comm_allgather_chain": (_i, [_P, _ll, _ll, _pd, _pll]),
     "olpe_comm_allreduce_moments": (_i, [_P, _pd]),
 }
 

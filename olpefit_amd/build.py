@@ -26,6 +26,17 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          "-Wall", "-Wno-unused-function"]
 
 
+def kernel_digest() -> str:
+    """16 hex digits over the device sources and flags: tags measured per-kernel
+    counts (profiles/valu_counts.json) with the code they were measured on."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for f in ("olpe.hip", "olpe_device.h", "exp_table.h"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build(lib: str = LIB) -> bool:
     if not os.path.exists(lib):
         return True

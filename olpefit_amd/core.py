@@ -240,6 +240,12 @@ class Sampler:
         check(self._lib.olpe_last_kernel_ms(self._ctx, C.byref(ms)))
         return float(ms.value)
 
+    def kernel_times(self, n: int):
+        """Durations (ms) of the last n sampler launches, oldest first (n <= 64)."""
+        out = np.empty(int(n))
+        check(self._lib.olpe_kernel_times(self._ctx, int(n), _dptr(out)))
+        return out
+
     # -- multi-GPU --------------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -256,6 +262,17 @@ class Sampler:
         out = np.empty((self.nranks * self.W, self.ps))
         check(self._lib.olpe_comm_allgather_state(self._ctx, _dptr(out)))
         return out
+
+    def allgather_chain(self, w0: int = 0, wn: int | None = None, out: bool = True):
+        """Chain concatenation over RCCL: walkers [w0, w0 + wn) of the last launch's
+        chain from every rank -> [nranks, wn, nrec, PS] (rank-major), or None with
+        ``out=False`` (gathered into the device buffer only: timing the collective)."""
+        wn = self.W - w0 if wn is None else wn
+        nrec = C.c_longlong(0)
+        buf = np.empty((self.nranks, wn, self._nrec, self.ps)) if out else None
+        check(self._lib.olpe_comm_allgather_chain(self._ctx, int(w0), int(wn), _dptr(buf),
+                                                  C.byref(nrec)))
+        return buf
 
     def allreduce_moments(self):
         out = np.empty(1 + 2 * self.ps)

@@ -711,6 +711,20 @@ int olpe_device_count(int *count) {
   return OLPE_OK;
 }
 
+int olpe_device_mem(int device, long long *free_bytes, long long *total_bytes) {
+  if (!free_bytes || !total_bytes) return set_err(OLPE_EINVAL, "NULL argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return set_err(OLPE_EHIP, "no HIP device visible");
+  if (device < 0 || device >= ndev) return set_err(OLPE_EINVAL, "bad device %d", device);
+  HIPCHK(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIPCHK(hipMemGetInfo(&f, &t));
+  *free_bytes = (long long)f;
+  *total_bytes = (long long)t;
+  return OLPE_OK;
+}
+
 int olpe_create(const void *image, int image_dtype, const void *pois2, double readnoise2,
                 const uint8_t *mask, int ny, int nx, int nsrc, int bkgd_mode, int device,
                 olpe_ctx **out) {
@@ -728,6 +742,26 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     return set_err(OLPE_EINVAL, "image_dtype must be OLPE_DTYPE_F32/F64");
   if (bkgd_mode != 0 && bkgd_mode != 1) return set_err(OLPE_EINVAL, "bkgd_mode must be 0/1");
   if (device < 0) return set_err(OLPE_EINVAL, "device must be a HIP ordinal (no CPU path)");
+  // stage image + 1/err in LDS when it fits beside a workgroup's wave slices (12 waves
+  // at 32x32 and 64x64, 16 for other sides; launch_gibbs_m)
+  const int np_ = nsrc == 2 ? 16 : 19;
+  const size_t npix_ = (size_t)nx * nx;
+  const bool lds_img = npix_ * sizeof(double2) +
+                           ((nx == 64 || nx == 32) ? 12 : 16) * wave_lds(nx, np_, true) +
+                           kEtabBytes <= 160 * 1024;
+  int wpb = 0;
+  if (const char *e = getenv("OLPE_WPB")) {                  // tuning experiments
+    // only the 64x64 LDS sampler has a choice (8 / 12 / 16 waves); its layout must fit
+    // the 160 KiB of LDS beside the cutout, or the launch would fail
+    wpb = atoi(e);
+    if (wpb != 8 && wpb != 12 && wpb != 16)
+      return set_err(OLPE_EINVAL, "OLPE_WPB=%s: must be 8, 12 or 16", e);
+    const size_t b = (size_t)wpb * wave_lds(nx, np_, true) + kEtabBytes + npix_ * sizeof(double2);
+    if (lds_img && nx == 64 && b > 160 * 1024)
+      return set_err(OLPE_EINVAL, "OLPE_WPB=%d needs %zu bytes of LDS at %dx%d (%d sources) > 163840",
+                     wpb, b, nx, nx, nsrc);
+    if (!(lds_img && nx == 64)) wpb = 0;     // no choice at other sides
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return set_err(OLPE_EHIP, "no HIP device visible");
@@ -744,10 +778,8 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   const size_t npix = (size_t)nx * nx;
   // stage image + 1/err in LDS when it fits beside a workgroup's wave slices (12 waves
   // at 32x32 and 64x64, 16 for other sides; launch_gibbs_m)
-  c->lds_img = npix * sizeof(double2) + ((nx == 64 || nx == 32) ? 12 : 16) * wave_lds(nx, c->np, true) +
-                   kEtabBytes <= 160 * 1024;
-  if (const char *e = getenv("OLPE_WPB")) c->wpb = atoi(e);   // tuning experiments
-
+  c->lds_img = lds_img;
+  c->wpb = wpb;
   std::vector<double2> hDE(npix), hDW(npix);
   for (size_t i = 0; i < npix; ++i) {
     const double d = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)image)[i]
@@ -769,8 +801,9 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     delete c;
     return set_err(OLPE_EHIP, "hipStreamCreate: %s", hipGetErrorString(e1));
   }
-  (void)hipEventCreate(&c->ev0);
-  (void)hipEventCreate(&c->ev1);
+  for (auto &pair : c->ev)
+    for (auto &ev : pair)
+      if (hipEventCreate(&ev) != hipSuccess) ev = nullptr;
   if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
       (rc = dev_alloc(&c->d_queue, 1))) {
     olpe_destroy(c);
@@ -801,11 +834,13 @@ void olpe_destroy(olpe_ctx *c) {
   olpe_comm_release(c);
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
-                  c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue};
+                  c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue,
+                  c->d_gather};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (auto &pair : c->ev)
+    for (auto &ev : pair)
+      if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -990,10 +1025,12 @@ int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_strid
   a.chain = c->d_chain;
   a.accept_min = accept_min;
   a.trace = c->trace_on ? c->d_trace : nullptr;
-  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  hipEvent_t *ev = c->ev[c->launches % olpe_ctx::kRing];
+  if (!ev[0] || !ev[1]) return set_err(OLPE_EHIP, "launch events were not created");
+  HIPCHK(hipEventRecord(ev[0], c->stream));
   if ((rc = launch_gibbs(c, a))) return rc;
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  c->timed = true;
+  HIPCHK(hipEventRecord(ev[1], c->stream));
+  ++c->launches;
   c->count = c1;
   if (nrec_out) *nrec_out = nrows;
   return OLPE_OK;
@@ -1142,15 +1179,26 @@ int olpe_sync(olpe_ctx *c) {
   return OLPE_OK;
 }
 
+int olpe_kernel_times(olpe_ctx *c, int n, double *ms_out) {
+  if (!c || !ms_out) return set_err(OLPE_EINVAL, "NULL argument");
+  if (n < 1 || n > olpe_ctx::kRing || n > c->launches)
+    return set_err(OLPE_EINVAL, "n = %d: 1..min(%d, launches so far = %lld)", n,
+                   olpe_ctx::kRing, c->launches);
+  HIPCHK(hipSetDevice(c->device));
+  for (int i = 0; i < n; ++i) {
+    hipEvent_t *ev = c->ev[(c->launches - n + i) % olpe_ctx::kRing];
+    HIPCHK(hipEventSynchronize(ev[1]));
+    float f = 0.f;
+    HIPCHK(hipEventElapsedTime(&f, ev[0], ev[1]));
+    ms_out[i] = f;
+  }
+  return OLPE_OK;
+}
+
 int olpe_last_kernel_ms(olpe_ctx *c, double *ms) {
   if (!c || !ms) return set_err(OLPE_EINVAL, "NULL argument");
-  if (!c->timed) return set_err(OLPE_ESTATE, "no sampler launch yet");
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipEventSynchronize(c->ev1));
-  float f = 0.f;
-  HIPCHK(hipEventElapsedTime(&f, c->ev0, c->ev1));
-  *ms = f;
-  return OLPE_OK;
+  if (!c->launches) return set_err(OLPE_ESTATE, "no sampler launch yet");
+  return olpe_kernel_times(c, 1, ms);
 }
 
 }  // extern "C"

@@ -4,7 +4,13 @@
 // reference's per-iteration comm.barrier() at apf_step2.py:338 carries no data).
 // The only exchange is at the end of a run:
 //   * all-gather of the final walker states      (ncclAllGather, rank-major)
+//   * all-gather of the chains (concatenation)   (ncclAllGather per walker range, so the
+//                                                 receive buffer is bounded by the range)
 //   * all-reduce of per-parameter moment sums    (ncclAllReduce, sum)
+// The reference's equivalent is one chain file per MPI rank behind the lockstep
+// barrier (apf_step2.py:338, :355-360).  RCCL gathers need equal counts on every rank:
+// each gather first all-reduces {W, -W, rows, -rows} (max) and returns OLPE_EINVAL on
+// every rank when the shards differ, instead of hanging or mixing rows.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -93,11 +99,36 @@ int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   return OLPE_OK;
 }
 
+// every rank has the same W and (if rows >= 0) the same chain rows; the verdict is
+// the same on every rank, so a mismatch is an error everywhere and nothing hangs
+static int check_uniform(olpe_ctx *c, long long rows) {
+  long long h[4] = {c->W, -(long long)c->W, rows, -rows};
+  long long *d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(h)));
+  hipError_t e = hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
+  ncclResult_t r = ncclSuccess;
+  if (e == hipSuccess) r = ncclAllReduce(d, d, 4, ncclInt64, ncclMax, (ncclComm_t)c->comm, c->stream);
+  if (e == hipSuccess && r == ncclSuccess)
+    e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
+  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+  if (e != hipSuccess) return set_err(OLPE_EHIP, "uniformity check: %s", hipGetErrorString(e));
+  if (h[0] != -h[1])
+    return set_err(OLPE_EINVAL, "walkers per rank differ (%lld..%lld): RCCL gathers need equal "
+                   "shards", -h[1], h[0]);
+  if (h[2] != -h[3])
+    return set_err(OLPE_EINVAL, "chain rows per rank differ (%lld..%lld)", -h[3], h[2]);
+  return OLPE_OK;
+}
+
 int olpe_comm_allgather_state(olpe_ctx *c, double *out) {
   if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
   if (!c->comm) return set_err(OLPE_ESTATE, "call olpe_comm_init first");
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
+  int rc;
+  if ((rc = check_uniform(c, 0))) return rc;
   const size_t per = (size_t)c->W * c->ps;
   double *d = nullptr;
   HIPCHK(hipMalloc(&d, per * c->nranks * sizeof(double)));
@@ -110,6 +141,40 @@ int olpe_comm_allgather_state(olpe_ctx *c, double *out) {
   (void)hipFree(d);
   if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
   if (e != hipSuccess) return set_err(OLPE_EHIP, "allgather copy: %s", hipGetErrorString(e));
+  return OLPE_OK;
+}
+
+int olpe_comm_allgather_chain(olpe_ctx *c, long long w0, long long wn, double *out,
+                              long long *nrec_out) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  if (!c->comm) return set_err(OLPE_ESTATE, "call olpe_comm_init first");
+  if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
+  HIPCHK(hipSetDevice(c->device));
+  int rc;
+  if ((rc = check_uniform(c, c->chain_rows))) return rc;
+  if (nrec_out) *nrec_out = c->chain_rows;
+  if (w0 < 0 || wn < 0 || w0 + wn > c->W)
+    return set_err(OLPE_EINVAL, "walker range [%lld, %lld) outside [0, %d)", w0, w0 + wn, c->W);
+  const size_t row = (size_t)c->chain_rows * c->ps;     // doubles per walker
+  const size_t per = (size_t)wn * row;                  // doubles per rank in this range
+  if (per == 0) return OLPE_OK;
+  const size_t need = per * c->nranks;
+  if (need > c->gather_cap) {
+    if (c->d_gather) (void)hipFree(c->d_gather);
+    c->d_gather = nullptr;
+    c->gather_cap = 0;
+    hipError_t e = hipMalloc(&c->d_gather, need * sizeof(double));
+    if (e != hipSuccess)
+      return set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the chain gather: %s (gather a "
+                     "smaller walker range)", need * sizeof(double), hipGetErrorString(e));
+    c->gather_cap = need;
+  }
+  NCCLCHK(ncclAllGather(c->d_chain + (size_t)w0 * row, c->d_gather, per, ncclDouble,
+                        (ncclComm_t)c->comm, c->stream));
+  if (out)
+    HIPCHK(hipMemcpyAsync(out, c->d_gather, need * sizeof(double), hipMemcpyDeviceToHost,
+                          c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return OLPE_OK;
 }
 

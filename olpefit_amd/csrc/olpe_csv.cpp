@@ -123,12 +123,21 @@ int olpe_csv_format(const double *rows, long long nrows, int ncols, int nan_row,
   return OLPE_OK;
 }
 
-int olpe_csv_write_chains(const char *const *paths, const double *chains, int nfiles,
-                          long long nrows, int ncols, int nan_row, int threads) {
-  if (!paths || nfiles < 0 || nrows < 0 || ncols <= 0 || (!chains && nrows > 0 && nfiles > 0))
-    return olpe::set_err(OLPE_EINVAL, "olpe_csv_write_chains: bad arguments");
+}  // extern "C"
+
+namespace {
+
+// Write (mode "wb") or append (mode "ab") file i <- rows [0, nrows) of
+// chains[i][rows_per_file][ncols], from a pool of threads; sizes_out[i] = the file's
+// size in bytes after the write (or NULL).
+int write_files(const char *fn, const char *const *paths, const double *chains, int nfiles,
+                long long rows_per_file, long long nrows, int ncols, bool nan_row, int threads,
+                const char *mode, long long *sizes_out) {
+  if (!paths || nfiles < 0 || nrows < 0 || rows_per_file < nrows || ncols <= 0 ||
+      (!chains && nrows > 0 && nfiles > 0))
+    return olpe::set_err(OLPE_EINVAL, "%s: bad arguments", fn);
   for (int i = 0; i < nfiles; ++i)
-    if (!paths[i]) return olpe::set_err(OLPE_EINVAL, "olpe_csv_write_chains: path %d is NULL", i);
+    if (!paths[i]) return olpe::set_err(OLPE_EINVAL, "%s: path %d is NULL", fn, i);
   unsigned nt = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
   if (nt == 0) nt = 1;
   if (nt > 64) nt = 64;
@@ -138,13 +147,22 @@ int olpe_csv_write_chains(const char *const *paths, const double *chains, int nf
     std::string s;
     for (int i = (int)t; i < nfiles; i += (int)nt) {
       s.clear();
-      format_rows(s, chains ? chains + (size_t)i * (size_t)nrows * (size_t)ncols : nullptr,
-                  nrows, ncols, nan_row != 0);
-      FILE *f = fopen(paths[i], "wb");
-      const bool ok = f && fwrite(s.data(), 1, s.size(), f) == s.size();
-      if (f && fclose(f) != 0) failed[t] = i;
-      if (!ok) failed[t] = i;
-      if (failed[t] >= 0) return;
+      format_rows(s, chains ? chains + (size_t)i * (size_t)rows_per_file * (size_t)ncols : nullptr,
+                  nrows, ncols, nan_row);
+      FILE *f = fopen(paths[i], mode);
+      bool ok = f && fwrite(s.data(), 1, s.size(), f) == s.size();
+      long long size = 0;
+      if (ok && sizes_out) {
+        ok = fflush(f) == 0 && fseek(f, 0, SEEK_END) == 0;
+        size = ok ? (long long)ftell(f) : -1;
+        ok = ok && size >= 0;
+      }
+      if (f && fclose(f) != 0) ok = false;
+      if (!ok) {
+        failed[t] = i;
+        return;
+      }
+      if (sizes_out) sizes_out[i] = size;
     }
   };
   std::vector<std::thread> pool;
@@ -152,9 +170,25 @@ int olpe_csv_write_chains(const char *const *paths, const double *chains, int nf
   work(0);
   for (auto &th : pool) th.join();
   for (unsigned t = 0; t < nt; ++t)
-    if (failed[t] >= 0)
-      return olpe::set_err(OLPE_EIO, "olpe_csv_write_chains: cannot write %s", paths[failed[t]]);
+    if (failed[t] >= 0) return olpe::set_err(OLPE_EIO, "%s: cannot write %s", fn, paths[failed[t]]);
   return OLPE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int olpe_csv_write_chains(const char *const *paths, const double *chains, int nfiles,
+                          long long nrows, int ncols, int nan_row, int threads) {
+  return write_files("olpe_csv_write_chains", paths, chains, nfiles, nrows, nrows, ncols,
+                     nan_row != 0, threads, "wb", nullptr);
+}
+
+int olpe_csv_append_chains(const char *const *paths, const double *chains, int nfiles,
+                           long long rows_per_file, long long nrows, int ncols, int threads,
+                           long long *sizes_out) {
+  return write_files("olpe_csv_append_chains", paths, chains, nfiles, rows_per_file, nrows,
+                     ncols, false, threads, "ab", sizes_out);
 }
 
 }  // extern "C"

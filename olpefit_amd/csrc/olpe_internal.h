@@ -14,8 +14,10 @@ struct olpe_ctx {
   bool lds_img = true; // cutout + 1/err staged in LDS by the sampler
   int wpb = 0;         // waves per workgroup of the 64x64 LDS sampler (0 = 12)
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  // start/stop events of the last kRing sampler launches (olpe_kernel_times)
+  static constexpr int kRing = 64;
+  hipEvent_t ev[kRing][2] = {};
+  long long launches = 0;
   double2 *d_DE = nullptr;   // [n*n] {data as f64, 1/err}, {0,0} where masked (EXACT)
   double2 *d_DW = nullptr;   // [n*n] {data/err, 1/err}, {0,0} where masked (FAST)
   // walker ensemble
@@ -50,6 +52,8 @@ struct olpe_ctx {
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;
+  double *d_gather = nullptr;   // receive buffer of olpe_comm_allgather_chain
+  size_t gather_cap = 0;
 };
 
 namespace olpe {

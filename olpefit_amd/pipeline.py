@@ -99,6 +99,56 @@ def write_chain_csvs(paths, chains, nan_row: bool = True, threads: int = 0) -> N
                                             int(nan_row), int(threads)))
 
 
+def append_chain_csvs(paths, chains, nrows=None, threads: int = 0) -> np.ndarray:
+    """Append rows [0, nrows) of ``chains[i]`` ([len(paths), rows, PS]) to file i --
+    the streaming form of the reference's every-10-iterations rewrite
+    (apf_step2.py:355-360) -- natively from a pool of threads
+    (olpe_csv_append_chains).  Returns each file's size in bytes afterwards."""
+    import ctypes as C
+    from . import _lib
+    from ._lib import check
+    chains = np.ascontiguousarray(np.asarray(chains, dtype=np.float64))
+    if chains.ndim != 3 or chains.shape[0] != len(paths):
+        raise ValueError(f"chains must be [len(paths), nrows, ncols], got {chains.shape}")
+    nrows = chains.shape[1] if nrows is None else int(nrows)
+    sizes = np.zeros(len(paths), dtype=np.int64)
+    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    check(_lib.load().olpe_csv_append_chains(
+        arr, chains.ctypes.data_as(C.POINTER(C.c_double)), len(paths), chains.shape[1], nrows,
+        chains.shape[2], int(threads), sizes.ctypes.data_as(C.POINTER(C.c_longlong))))
+    return sizes
+
+
+NPY_HEADER = 128
+
+
+def npy_header(rows: int, cols: int) -> bytes:
+    """A fixed-size (128-byte) .npy v1.0 header for a C-order float64 [rows, cols]
+    array, so that a chain file can grow in place: append rows, rewrite the header."""
+    d = "{'descr': '<f8', 'fortran_order': False, 'shape': (%d, %d), }" % (rows, cols)
+    body = d.encode("latin1")
+    pad = NPY_HEADER - 10 - len(body) - 1
+    if pad < 0:
+        raise ValueError("chain too large for the fixed .npy header")
+    return b"\x93NUMPY\x01\x00" + np.uint16(NPY_HEADER - 10).tobytes() + body + b" " * pad + b"\n"
+
+
+def append_npy_chains(paths, chains, nrows, rows_before: int) -> None:
+    """``{w}_chain.npy`` sidecars grown by one launch: rows [0, nrows) of chains[i] are
+    appended after ``rows_before`` rows and the header rewritten (each file stays a
+    valid .npy between launches)."""
+    chains = np.asarray(chains, dtype=np.float64)
+    cols = chains.shape[2]
+    for i, path in enumerate(paths):
+        mode = "r+b" if os.path.exists(path) else "w+b"
+        with open(path, mode) as f:
+            f.seek(NPY_HEADER + rows_before * cols * 8)
+            f.truncate()
+            f.write(np.ascontiguousarray(chains[i, :nrows]).tobytes())
+            f.seek(0)
+            f.write(npy_header(rows_before + nrows, cols))
+
+
 def write_chain_csv(path: str, rows) -> None:
     """One ``{rank}_finalarray_mpi.csv``: ``rows`` must already hold the NaN seed row."""
     rows = np.atleast_2d(np.asarray(rows, dtype=np.float64))

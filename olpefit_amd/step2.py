@@ -1,29 +1,42 @@
 """apf_step2 command line: the reference's CLI and file surface over the GPU sampler.
 
-Reference: apf_step2.py (2 sources) and 3body/apf_step2_3body.py (3 sources).  Kept:
-positional ``image``, ``-i {1,2a}`` (2-source only), the output directory
-``<dir>/<frame>_apf_results/``, ``{w}_finalarray_mpi.csv`` (NaN first row, PS columns,
-rows from count == burn_in, written up to the last multiple of 10) and
-``{w}_acceptance_rate.csv`` per walker w (the reference's MPI rank), and the run-length
-semantics: the run ends at the first iteration where some walker has tried every
-parameter ``accept_min`` times (apf_step2.py:300 + the lockstep barrier at :338).
+Reference: apf_step2.py (2 sources), 3body/apf_step2_3body.py (3 sources) and
+apf_step2a.py (the single-walker warm-up).  Kept: positional ``image``, ``-i {1,2a}``
+(2-source only), the output directory ``<dir>/<frame>_apf_results/``,
+``{w}_finalarray_mpi.csv`` (NaN first row, PS columns, rows from count == burn_in,
+written up to the last multiple of 10) and ``{w}_acceptance_rate.csv`` per walker w
+(the reference's MPI rank), and the run-length semantics: the run ends at the first
+iteration where some walker has tried every parameter ``accept_min`` times
+(apf_step2.py:300 + the lockstep barrier at :338).
+
+Output is streamed.  The reference rewrites every file each 10 iterations
+(apf_step2.py:355-365), so a killed run leaves its chains on disk; here each kernel
+launch (a *chunk*, a multiple of 10 iterations) appends its rows to the per-walker
+files and rewrites the acceptance files, so the files always hold what the
+reference's files hold at that count, host memory is bounded by one chunk, and a
+checkpoint (walker state, counters, RNG streams, file sizes) after each chunk makes a
+killed run resumable (``--resume``) with the same chains as an uninterrupted one.
 
 Added flags: ``--walkers`` (the reference's MPI size), ``--seed``, ``--iters`` (fixed
 length instead of accept_min), ``--record-stride``, ``--gpus``, ``--exact``,
-``--fixed-bkgd``, ``--chunk``, ``--no-csv``, ``--npy``.
+``--fixed-bkgd``, ``--chunk``, ``--mem-budget``, ``--checkpoint-every``, ``--resume``,
+``--no-csv``, ``--npy``.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
+import json
 import os
 import sys
 import threading
-import time
 
 import numpy as np
 
-from . import fitsio, pipeline
+from . import _lib, fitsio, pipeline
 from .core import Sampler
+
+MAX_CHUNK = 20000          # iterations per launch when memory allows
 
 
 def parse(argv, nsrc, variant="2"):
@@ -43,8 +56,9 @@ def parse(argv, nsrc, variant="2"):
     ap.add_argument("--burn-in", type=int,
                     default=6000 if (nsrc == 2 and variant == "2") else 0)
     ap.add_argument("--iters", type=int, default=0 if variant == "2" else 5000,
-                    help="run exactly this many iterations (overrides --accept-min; use a "
-                         "multiple of 10 to mirror the reference's write cadence)")
+                    help="run exactly this many iterations (overrides --accept-min); the "
+                         "files hold rows up to the last multiple of 10, as the "
+                         "reference's (apf_step2.py:355)")
     ap.add_argument("--seed", type=int, default=None,
                     help="walker w uses np.random.seed(seed + w) (default: OS entropy)")
     ap.add_argument("--record-stride", type=int, default=1)
@@ -53,11 +67,25 @@ def parse(argv, nsrc, variant="2"):
     ap.add_argument("--exact", action="store_true", help="exact per-pixel exp evaluation")
     ap.add_argument("--fixed-bkgd", action="store_true",
                     help="background = p[9] instead of the reference's p[12] (2-source)")
-    ap.add_argument("--chunk", type=int, default=20000, help="iterations per kernel launch")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="iterations per kernel launch (rounded up to a multiple of 10; "
+                         f"default: as many as --mem-budget allows, at most {MAX_CHUNK})")
+    ap.add_argument("--mem-budget", type=float, default=1.0,
+                    help="GiB of chain rows per launch (host copy; the device buffer is "
+                         "also kept under a quarter of free device memory)")
+    ap.add_argument("--checkpoint-every", type=int, default=1,
+                    help="write a resumable checkpoint every N launches (0 = never)")
+    ap.add_argument("--resume", action="store_true",
+                    help="continue the run recorded in the output directory's checkpoint")
     ap.add_argument("--no-csv", action="store_true")
     ap.add_argument("--npy", action="store_true", help="also write {w}_chain.npy")
     ap.add_argument("-q", "--quiet", action="store_true")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if variant == "2a" and args.walkers != 1:
+        ap.error("apf_step2a runs one walker (it writes a single step2a.csv)")
+    if args.walkers < 1 or args.record_stride < 1 or args.chunk < 0:
+        ap.error("--walkers and --record-stride must be >= 1, --chunk >= 0")
+    return args
 
 
 class Shard:
@@ -67,6 +95,7 @@ class Shard:
         self.s = Sampler(img, hdr["ITIME"], hdr["COADDS"], hdr["MULTISAM"], hdr["SAMPMODE"],
                          nsrc=nsrc, bkgd_mode=bkgd_mode, device=device)
         self.s.set_eval_mode("exact" if exact else "fast")
+        self.device = device
         self.w0, self.W = w0, W
         p = p0.copy()
         with np.errstate(all="ignore"):
@@ -74,7 +103,7 @@ class Shard:
         self.p_init = p
         self.s.seed(seeds[w0:w0 + W])
         self.s.set_state(np.tile(p, (W, 1)))
-        self.chunks = []
+        self.last = None                 # the last launch's chain [W, nrec, PS]
 
     def snapshot(self):
         return self.s.get_state(), self.s.rng_state(), self.s.count
@@ -87,12 +116,7 @@ class Shard:
 
     def run(self, n, burn_in, stride, accept_min):
         chain = self.s.run(n, burn_in=burn_in, record_stride=stride, accept_min=accept_min)
-        self.chunks.append(chain if chain is not None else np.zeros((self.W, 0, self.s.ps)))
-
-    def chain(self):
-        if not self.chunks:
-            return np.zeros((self.W, 0, self.s.ps))
-        return np.concatenate(self.chunks, axis=1)
+        self.last = chain if chain is not None else np.zeros((self.W, 0, self.s.ps))
 
 
 def _parallel(shards, fn):
@@ -112,25 +136,161 @@ def _parallel(shards, fn):
         raise errs[0]
 
 
+def device_free_bytes(device: int) -> int:
+    f, t = C.c_longlong(0), C.c_longlong(0)
+    _lib.check(_lib.load().olpe_device_mem(int(device), C.byref(f), C.byref(t)))
+    return int(f.value)
+
+
+def chunk_size(shards, stride: int, requested: int, budget_gib: float) -> int:
+    """Iterations per launch: ``requested`` (rounded up to a multiple of 10), or the
+    largest multiple of 10 (<= MAX_CHUNK) whose chain rows -- W x (n/stride + 1) x PS x
+    8 bytes -- fit the host budget over all shards and a quarter of each device's free
+    memory.  At 65,536 walkers and stride 1 that is a few hundred iterations."""
+    if requested:
+        return max(10, ((requested + 9) // 10) * 10)
+    ps = shards[0].s.ps
+    host_rows = budget_gib * 2 ** 30 / (sum(sh.W for sh in shards) * ps * 8)
+    dev_rows = min(device_free_bytes(sh.device) / 4 / (sh.W * ps * 8) for sh in shards)
+    rows = max(1.0, min(host_rows, dev_rows) - 1)
+    n = int(rows * stride) // 10 * 10
+    return int(min(MAX_CHUNK, max(10, n)))
+
+
+class Output:
+    """The per-walker files of one run: chain CSVs (+ optional .npy sidecars) grown by
+    each launch, acceptance files rewritten at each launch, and the checkpoint."""
+
+    def __init__(self, outdir, shards, variant, csv, npy):
+        self.outdir, self.shards, self.csv, self.npy = outdir, shards, csv, npy
+        if variant == "2":
+            self.names = [[(f"{sh.w0 + k}_finalarray_mpi.csv", f"{sh.w0 + k}_acceptance_rate.csv")
+                           for k in range(sh.W)] for sh in shards]
+        else:                                   # apf_step2a.py:320-331 (one walker)
+            self.names = [[("step2a.csv", "step2a_acceptance_rate")] for _ in shards]
+        self.npy_names = [[f"{sh.w0 + k}_chain.npy" for k in range(sh.W)] for sh in shards]
+        self.sizes = [np.zeros(sh.W, dtype=np.int64) for sh in shards]
+        self.npy_rows = 0
+
+    def _paths(self, g, which):
+        return [self.outdir + n[which] for n in self.names[g]]
+
+    def start(self):
+        """The NaN seed row (apf_step2.py:278-279) of every chain file."""
+        for g, sh in enumerate(self.shards):
+            if self.csv:
+                empty = np.zeros((sh.W, 0, sh.s.ps))
+                pipeline.write_chain_csvs(self._paths(g, 0), empty, nan_row=True)
+                self.sizes[g] = np.array([os.path.getsize(p) for p in self._paths(g, 0)])
+            if self.npy:
+                pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
+                                           np.zeros((sh.W, 0, sh.s.ps)), 0, 0)
+
+    def truncate(self, sizes, npy_rows):
+        """Back to a checkpoint: rows appended after it are dropped (they are re-run)."""
+        for g, sh in enumerate(self.shards):
+            if self.csv:
+                for p, n in zip(self._paths(g, 0), sizes[sh.w0:sh.w0 + sh.W]):
+                    with open(p, "r+b") as f:
+                        f.truncate(int(n))
+                self.sizes[g] = np.array(sizes[sh.w0:sh.w0 + sh.W], dtype=np.int64)
+        if self.npy:
+            for g, sh in enumerate(self.shards):
+                pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
+                                           np.zeros((sh.W, 0, sh.s.ps)), 0, npy_rows)
+        self.npy_rows = npy_rows
+
+    def commit(self, acceptance=True):
+        """Append every shard's last launch and rewrite the acceptance files
+        (str(total_accept / total_tries), apf_step2.py:362-365; the reference writes
+        them only once count >= burn_in, :342)."""
+        def body(g):
+            sh = self.shards[g]
+            rows = sh.last.shape[1]
+            _, tries, acc = sh.s.get_state()
+            if self.csv:
+                if rows:
+                    # one writer thread per shard for step 2a, where the files are shared
+                    self.sizes[g] = pipeline.append_chain_csvs(self._paths(g, 0), sh.last)
+                if acceptance:
+                    for k, p in enumerate(self._paths(g, 1)):
+                        pipeline.write_acceptance(p, acc[k], tries[k])
+            if self.npy and rows:
+                pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
+                                           sh.last, rows, self.npy_rows)
+            return rows
+        rows = [0] * len(self.shards)
+
+        def run(sh):
+            g = self.shards.index(sh)
+            rows[g] = body(g)
+        _parallel(self.shards, run)
+        self.npy_rows += rows[0]
+
+    def all_sizes(self):
+        return np.concatenate(self.sizes)
+
+
+def checkpoint_path(outdir, variant):
+    return outdir + ("step2_checkpoint.npz" if variant == "2" else "step2a_checkpoint.npz")
+
+
+def save_checkpoint(path, shards, out, count, config):
+    st, tr, ac, mt, ga = [], [], [], [], []
+    for sh in shards:
+        s, t, a = sh.s.get_state()
+        m, g = sh.s.rng_state()
+        st.append(s), tr.append(t), ac.append(a), mt.append(m), ga.append(g)
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, state=np.concatenate(st), tries=np.concatenate(tr),
+             accepts=np.concatenate(ac), mt=np.concatenate(mt), gauss=np.concatenate(ga),
+             count=np.int64(count), csv_sizes=out.all_sizes(), npy_rows=np.int64(out.npy_rows),
+             config=np.array(json.dumps(config, sort_keys=True)))
+    os.replace(tmp, path)
+
+
+def load_checkpoint(path):
+    with np.load(path, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
 def main(argv=None, nsrc=2, variant="2"):
     """variant "2": apf_step2 (many walkers, {w}_finalarray_mpi.csv); "2a": the single
     walker warm-up of apf_step2a.py writing step2a.csv / step2a_acceptance_rate
-    (:324-331), which ``apf_step2.py -i 2a`` then starts from (apf_step2.py:248-256)."""
+    (:320-331), which ``apf_step2.py -i 2a`` then starts from (apf_step2.py:248-256)."""
     args = parse(sys.argv[1:] if argv is None else argv, nsrc, variant)
     say = (lambda *a: None) if args.quiet else print
     image, hdr = fitsio.getdata_header(args.image)              # apf_step2.py:160-161
     directory, frame, outdir = pipeline.image_paths(args.image)  # :164-170
     say(outdir)
     os.makedirs(outdir, exist_ok=True)                           # :172-173
-    if getattr(args, "initial_guess_option", None) == "2a":      # :248-256
-        say("I am taking the initial guess from Step 2a output")
-        p0 = pipeline.read_step2a(outdir + "step2a.csv")
+    ckpt = checkpoint_path(outdir, variant)
+    resume = load_checkpoint(ckpt) if args.resume else None
+    if args.resume and resume is None:
+        raise FileNotFoundError(ckpt)
+    config = {"image": os.path.abspath(args.image), "nsrc": nsrc, "variant": variant,
+              "walkers": args.walkers, "accept_min": args.accept_min, "burn_in": args.burn_in,
+              "iters": args.iters, "stride": args.record_stride, "exact": args.exact,
+              "fixed_bkgd": args.fixed_bkgd, "csv": not args.no_csv, "npy": args.npy}
+    if resume is not None:
+        old = json.loads(str(resume["config"]))
+        base, p0 = old.pop("seed"), np.array(old.pop("p0"))
+        if old != config:
+            diff = {k: (old.get(k), config.get(k)) for k in set(old) | set(config)
+                    if old.get(k) != config.get(k)}
+            raise ValueError(f"--resume: the checkpoint was written with other settings {diff}")
+        say(f"Resuming from {ckpt} at count {int(resume['count'])}")
     else:
-        say("I am taking the initial guess from Step 1 output")
-        guess = pipeline.read_guess(directory + frame + "_initialguess")
-        p0 = pipeline.initial_parameters(image, guess, nsrc)
+        if getattr(args, "initial_guess_option", None) == "2a":  # :248-256
+            say("I am taking the initial guess from Step 2a output")
+            p0 = pipeline.read_step2a(outdir + "step2a.csv")
+        else:
+            say("I am taking the initial guess from Step 1 output")
+            guess = pipeline.read_guess(directory + frame + "_initialguess")
+            p0 = pipeline.initial_parameters(image, guess, nsrc)
+        base = args.seed if args.seed is not None else int.from_bytes(os.urandom(4), "little")
+    config.update(seed=base, p0=[float(v) for v in p0])
     W = args.walkers
-    base = args.seed if args.seed is not None else int.from_bytes(os.urandom(4), "little")
     seeds = (base + np.arange(W, dtype=np.int64)) & 0xFFFFFFFF
     say(f"walkers {W}, seeds {base}..{base + W - 1} (np.random.seed semantics)")
     ng = max(1, min(args.gpus, W))
@@ -140,59 +300,72 @@ def main(argv=None, nsrc=2, variant="2"):
     say("Found initial chi-squared:", shards[0].p_init[-1])
     say("Initial guess:", shards[0].p_init)
 
+    out = Output(outdir, shards, variant, csv=not args.no_csv, npy=args.npy)
+    count = 0
+    if resume is not None:
+        count = int(resume["count"])
+        for sh in shards:
+            sl = slice(sh.w0, sh.w0 + sh.W)
+            sh.restore(((resume["state"][sl], resume["tries"][sl], resume["accepts"][sl]),
+                        (resume["mt"][sl], resume["gauss"][sl]), count))
+        out.truncate(resume["csv_sizes"], int(resume["npy_rows"]))
+    else:
+        out.start()
+
     burn, stride = args.burn_in, args.record_stride
-    t0 = time.perf_counter()
+    chunk = chunk_size(shards, stride, args.chunk, args.mem_budget)
+    launches = 0
+
+    def commit():
+        nonlocal launches
+        out.commit(acceptance=count >= burn)
+        launches += 1
+        if args.checkpoint_every and launches % args.checkpoint_every == 0:
+            save_checkpoint(ckpt, shards, out, count, config)
+
+    def run(n, accept_min=0, record=True):
+        _parallel(shards, lambda sh: sh.run(n, burn, stride if record else 0, accept_min))
+
     if args.iters:
-        total = args.iters
-        done = 0
-        while done < total:
-            n = min(args.chunk, total - done)
-            _parallel(shards, lambda sh: sh.run(n, burn, stride, 0))
-            done += n
-            say("Loop count:", done)
-        stop = total
+        # the files hold rows up to L = the last multiple of 10 <= iters (:355); the
+        # iterations after L change no file
+        last = (args.iters // 10) * 10
+        while count < last:
+            n = min(chunk, last - count)
+            run(n)
+            count += n
+            commit()
+            say("Loop count:", count)
+        if args.iters > max(count, last):
+            run(args.iters - max(count, last), record=False)
     else:
         # accept_min semantics: the run ends at the first count C where some walker has
         # min(total_tries) >= accept_min (apf_step2.py:300); with the lockstep barrier
         # every file then holds rows up to L = the last multiple of 10 <= C (:355).
-        # Chunks start at multiples of 10, so L lies inside the chunk that found C: that
-        # chunk is re-run from its snapshot (RNG included, hence identical) up to L.
-        chunk = ((args.chunk + 9) // 10) * 10
-        done = 0
-        stop = None
-        while stop is None:
+        # Launches start at multiples of 10, so L lies inside the launch that found C:
+        # that launch is re-run from its snapshot (RNG included, hence identical) up to L.
+        while True:
             snaps = [sh.snapshot() for sh in shards]
-            _parallel(shards, lambda sh: sh.run(chunk, burn, stride, args.accept_min))
-            done += chunk
+            run(chunk, args.accept_min)
             hits = np.concatenate([sh.s.done_at() for sh in shards])
             hits = hits[hits >= 0]
-            say("Loop count:", done)
-            if hits.size:
-                stop = (int(hits.min()) // 10) * 10
-                for sh, sn in zip(shards, snaps):
-                    sh.chunks.pop()
-                    sh.restore(sn)
-                rest = stop - (done - chunk)
-                if rest > 0:
-                    _parallel(shards, lambda sh: sh.run(rest, burn, stride, 0))
-    # files (apf_step2.py:355-365): NaN first row + the recorded rows, acceptance =
-    # str(total_accept / total_tries) at the final count
+            if not hits.size:
+                count += chunk
+                commit()
+                say("Loop count:", count)
+                continue
+            stop = (int(hits.min()) // 10) * 10
+            for sh, sn in zip(shards, snaps):
+                sh.restore(sn)
+            if stop > count:
+                run(stop - count)
+                count = stop
+                commit()
+            say("Loop count:", count)
+            break
+    if os.path.exists(ckpt):
+        os.remove(ckpt)                  # the run is complete: nothing to resume
     for sh in shards:
-        chain = sh.chain()
-        _, tries, acc = sh.s.get_state()
-        if not args.no_csv:
-            names = [(f"{sh.w0 + k}_finalarray_mpi.csv", f"{sh.w0 + k}_acceptance_rate.csv")
-                     if variant == "2" else ("step2a.csv", "step2a_acceptance_rate")
-                     for k in range(sh.W)]
-            # chain files: native formatter + writer threads (libolpe olpe_csv_*)
-            # (step 2a names one file for every walker: written in order, the last wins)
-            pipeline.write_chain_csvs([outdir + c for c, _ in names],
-                                      chain.reshape(sh.W, -1, chain.shape[-1]),
-                                      threads=0 if variant == "2" else 1)
-            for k, (_, acc_name) in enumerate(names):
-                pipeline.write_acceptance(outdir + acc_name, acc[k], tries[k])
-        if args.npy:
-            for k in range(sh.W):
-                np.save(outdir + f"{sh.w0 + k}_chain.npy", chain[k])
+        sh.s.close()
     say("done with loop")
     return outdir

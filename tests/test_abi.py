@@ -82,3 +82,26 @@ def test_null_arguments_are_errors(lib):
     assert lib.olpe_run(None, 1, 0, 1, 0, None) == _lib.EINVAL
     assert lib.olpe_sync(None) == _lib.EINVAL
     lib.olpe_destroy(None)
+
+
+def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):
+    """OLPE_WPB (a tuning knob) is checked in olpe_create against the 160 KiB LDS before
+    anything touches a GPU: 16 waves of the 64x64 sampler (with its draw tables) do not
+    fit beside the cutout, so the launch would fail; 7 is not a workgroup size."""
+    img = np.ones((64, 64), np.float32)
+    ctx = C.c_void_p()
+
+    def create(nsrc=2):
+        return lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 64, 64, nsrc,
+                               0, 0, C.byref(ctx))
+    monkeypatch.setenv("OLPE_WPB", "16")
+    assert create() == _lib.EINVAL
+    msg = lib.olpe_last_error().decode()
+    assert "bytes of LDS" in msg and int(re.search(r"needs (\d+) bytes", msg).group(1)) > 163840
+    monkeypatch.setenv("OLPE_WPB", "7")
+    assert create() == _lib.EINVAL and b"8, 12 or 16" in lib.olpe_last_error()
+    monkeypatch.setenv("OLPE_WPB", "12")
+    n = C.c_int(0)
+    lib.olpe_device_count(C.byref(n))
+    if not n.value:
+        assert create() == _lib.EHIP            # valid knob: fails only for lack of a GPU

@@ -47,7 +47,7 @@ def test_cli_multi_walker_files_feed_step3(tmp_path):
     assert abs(s["xcs"]["mean"] - synth.truth_params(32)[0]) < 0.5
 
 
-def test_cli_seeds_are_gpu_count_independent(tmp_path):
+def test_cli_seeds_are_gpu_count_independent(tmp_path, monkeypatch):
     """Seeds come from the global walker index, so a sharded run (two contexts on the
     same GPU here) writes the same chains as a single-context run."""
     path = synth.write_case(str(tmp_path / "a"), 32, 2)
@@ -55,34 +55,135 @@ def test_cli_seeds_are_gpu_count_independent(tmp_path):
                       "-q", "--no-csv", "--npy"])
     one = [np.load(out + f"{w}_chain.npy") for w in range(5)]
     path2 = synth.write_case(str(tmp_path / "b"), 32, 2)
-    from olpefit_amd.core import Sampler  # noqa: F401
-    import olpefit_amd.step2 as s2
-    args = [path2, "--walkers", "5", "--seed", "11", "--iters", "200", "--burn-in", "0", "-q",
-            "--no-csv", "--npy", "--gpus", "2"]
-    orig = s2.Shard.__init__
-
-    def same_device(self, img, hdr, nsrc, device, *a, **k):     # 2 shards, 1 physical GPU
-        orig(self, img, hdr, nsrc, 0, *a, **k)
-    s2.Shard.__init__ = same_device
-    try:
-        out2 = s2.main(args)
-    finally:
-        s2.Shard.__init__ = orig
+    _same_device_shards(monkeypatch)                         # 2 shards, 1 physical GPU
+    out2 = step2.main([path2, "--walkers", "5", "--seed", "11", "--iters", "200", "--burn-in",
+                       "0", "-q", "--no-csv", "--npy", "--gpus", "2"])
     for w in range(5):
         np.testing.assert_array_equal(np.load(out2 + f"{w}_chain.npy"), one[w])
 
 
-def test_step2a_then_step2_from_2a(tmp_path):
-    """apf_step2a writes step2a.csv (one walker, 5000 steps by default; 300 here);
-    apf_step2 -i 2a starts every walker from its last row (apf_step2.py:248-256)."""
+def _oracle_walkers(n, nsrc, seeds, iters):
+    from oracle import olpe_oracle as ora
+    img, _ = synth.make_image(n, nsrc, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = ora.initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    out = []
+    for sd in seeds:
+        w = ora.Walker(dm, err, p0, int(sd), nsrc)
+        w.init_chi2()
+        chain, _ = w.run(iters)
+        out.append((chain, w))
+    return out
+
+
+def test_step2a_matches_oracle_then_step2_from_2a(tmp_path):
+    """apf_step2a (reference apf_step2a.py:271-331): one walker, n_steps iterations, rows
+    from count 1 written up to the last multiple of 10 (305 -> 300 rows), acceptance
+    text str(total_accept / total_tries) at count 300 -- against the oracle walker with
+    the same seed (values rel 1e-9, FAST eval; acceptance text identical).  Then
+    apf_step2 -i 2a starts every walker from step2a.csv's last row
+    (apf_step2.py:248-256)."""
     path = synth.write_case(str(tmp_path), 32, 2)
-    out = step2.main([path, "--iters", "300", "--seed", "5", "-q"], nsrc=2, variant="2a")
+    out = step2.main([path, "--iters", "305", "--seed", "5", "-q"], nsrc=2, variant="2a")
     a = np.genfromtxt(out + "step2a.csv", delimiter=",")
     assert a.shape == (301, 17) and np.all(np.isnan(a[0]))
-    assert os.path.exists(out + "step2a_acceptance_rate")
+    (ref, w), = _oracle_walkers(32, 2, [5], 300)
+    np.testing.assert_allclose(a[1:], ref, rtol=1e-9, atol=0)
+    with open(out + "step2a_acceptance_rate") as f:
+        assert f.read() == pipeline.acceptance_text(w.total_accept, w.total_tries)
+    assert not os.path.exists(out + "step2a_checkpoint.npz")      # removed when complete
     out2 = step2.main([path, "-i", "2a", "--walkers", "3", "--iters", "20", "--burn-in", "0",
                        "--seed", "9", "-q", "--no-csv", "--npy"])
     c0 = np.load(out2 + "0_chain.npy")
+    assert c0.shape == (20, 17)
     # the first row differs from step2a's last row in at most one parameter + chi^2
     diff = np.nonzero(c0[0, :16] != a[-1, :16])[0]
     assert diff.size <= 1
+
+
+def _same_device_shards(monkeypatch):
+    """--gpus N on the one-GPU box: every shard's context on device 0."""
+    orig = step2.Shard.__init__
+
+    def same_device(self, img, hdr, nsrc, device, *a, **k):
+        orig(self, img, hdr, nsrc, 0, *a, **k)
+    monkeypatch.setattr(step2.Shard, "__init__", same_device)
+
+
+@pytest.mark.parametrize("gpus,extra", [(1, ["--chunk", "30"]), (2, ["--chunk", "30"]),
+                                        (1, ["--mem-budget", "0.0001"])])
+def test_cli_accept_min_multi_walker_stop(tmp_path, golden, monkeypatch, gpus, extra):
+    """accept_min with several walkers (apf_step2.py:300 + the lockstep barrier at :338):
+    the run ends at the global earliest count C at which some walker has tried every
+    parameter accept_min times, and every file holds rows burn_in..L, L = the last
+    multiple of 10 <= C (:355).  The reference's own per-walker trajectories
+    (tests/golden/c32.npz: 4 seeds, each run to its own accept_min) give the expected
+    rows and acceptance counters; two shards (two contexts on the one GPU) must write
+    the same files, and so must a launch size set by the memory budget."""
+    g = golden("c32")
+    C = int(g["traj_len"].min())
+    L = (C // 10) * 10
+    burn = int(g["burn_in"])
+    if gpus > 1:
+        _same_device_shards(monkeypatch)
+    path = synth.write_case(str(tmp_path), 32, 2)
+    out = step2.main([path, "--walkers", "4", "--seed", "1000", "--accept-min",
+                      str(int(g["accept_min"])), "--burn-in", str(burn), "--gpus", str(gpus),
+                      "-q", *extra])
+    for w in range(4):
+        got = np.genfromtxt(out + f"{w}_finalarray_mpi.csv", delimiter=",")
+        assert got.shape == (L - burn + 2, 17)
+        np.testing.assert_allclose(got[1:], g["traj_params"][w][burn - 1:L], rtol=1e-9)
+        r = g["traj_r"][w][:L]
+        tries = np.bincount(r, minlength=16).astype(float)
+        acc = np.bincount(r[g["traj_acc"][w][:L].astype(bool)], minlength=16).astype(float)
+        with open(out + f"{w}_acceptance_rate.csv") as f:
+            assert f.read() == pipeline.acceptance_text(acc, tries)
+
+
+def test_cli_three_source_feeds_step3(tmp_path):
+    """3body/apf_step2_3body.py -> step 3 (3body/apf_step3_3body.py:169-189 read, 20
+    columns; GR :292-310 with Python-2 RC = sqrt(PSRF)); chains against the oracle."""
+    path = synth.write_case(str(tmp_path), 32, 3)
+    out = step2.main([path, "--walkers", "3", "--seed", "40", "--iters", "120", "-q"], nsrc=3)
+    c = step3.load_chains(out, 3, additional_burnin=1)
+    assert c.shape == (120, 3, 20)
+    for w, (ref, _) in enumerate(_oracle_walkers(32, 3, [40, 41, 42], 120)):
+        np.testing.assert_allclose(c[:, w, :], ref, rtol=1e-9)
+    s = step3.summary(c, nsrc=3)
+    assert list(s) == step3.NAMES_3[:-1]
+    for name in s:
+        assert s[name]["gr_rc"] == np.sqrt(s[name]["gr_psrf"]) or np.isnan(s[name]["gr_rc"])
+
+
+@pytest.mark.parametrize("mode", ["iters", "accept_min"])
+def test_cli_resume_after_interrupt(tmp_path, monkeypatch, mode):
+    """A run killed after a launch's rows reached the files but before its checkpoint
+    was written resumes (--resume) from the previous checkpoint: the files are cut back
+    to the checkpoint's sizes, the launch is re-run from the saved walker state and RNG
+    streams, and every file ends byte-equal to an uninterrupted run's."""
+    path = synth.write_case(str(tmp_path / "ref"), 32, 2)
+    path2 = synth.write_case(str(tmp_path / "cut"), 32, 2)
+    run = ["--walkers", "3", "--seed", "21", "--burn-in", "15", "--chunk", "40", "--npy", "-q"]
+    run += ["--iters", "205"] if mode == "iters" else ["--accept-min", "25"]
+    ref = step2.main([path, *run])
+    calls = {"n": 0}
+    orig = step2.save_checkpoint
+
+    def dying(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise KeyboardInterrupt("killed")
+        orig(*a, **k)
+    monkeypatch.setattr(step2, "save_checkpoint", dying)
+    with pytest.raises(KeyboardInterrupt):
+        step2.main([path2, *run])
+    monkeypatch.setattr(step2, "save_checkpoint", orig)
+    cut = step2.main([path2, *run, "--resume"])
+    for w in range(3):
+        for name in (f"{w}_finalarray_mpi.csv", f"{w}_acceptance_rate.csv"):
+            with open(ref + name, "rb") as f, open(cut + name, "rb") as h:
+                assert f.read() == h.read(), name
+        np.testing.assert_array_equal(np.load(cut + f"{w}_chain.npy"),
+                                      np.load(ref + f"{w}_chain.npy"))
+    assert not os.path.exists(cut + "step2_checkpoint.npz")

@@ -1,24 +1,17 @@
-"""The N>1 path on CPU: two gloo ranks run the host orchestration of bench.py /
-olpefit_amd.dist (shard ranges, global-index seeds, barrier, max-over-ranks timing,
-id broadcast) with the oracle standing in for the per-GPU sampler, and the gathered
-per-rank chains equal a single-process run of all walkers (chains do not depend on
-the number of GPUs)."""
+"""The N>1 path on CPU: two (and three) ranks run the host orchestration of bench.py
+/ olpefit_amd.dist -- the torch-free TCP host group (rendezvous next to a port that is
+already taken, as torchrun's agent store takes MASTER_PORT), shard ranges,
+global-index seeds, barrier, max/sum over ranks, id broadcast -- with the oracle
+standing in for the per-GPU sampler, and the gathered per-rank chains equal a
+single-process run of all walkers (chains do not depend on the number of GPUs)."""
+import multiprocessing as mp
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 from olpefit_amd import dist as odist
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _oracle_chains(seeds, n_iters):
@@ -38,38 +31,45 @@ def _oracle_chains(seeds, n_iters):
 def _rank_main(rank, world, port, total, n_iters, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    import torch.distributed as dist
+    import sys
     r, w, _ = odist.env()
-    g = odist.HostGroup(r, w)
+    g = odist.HostGroup(r, w, timeout_s=120)
     w0, n = odist.shard(total, w, r)
     seeds = odist.walker_seeds(1000, w0, n)
     uid = g.broadcast(b"x" * 128 if r == 0 else None)
     g.barrier()
     chains = _oracle_chains(seeds, n_iters)
     t = g.allmax(float(r + 1))
-    gathered = [None] * w
-    dist.all_gather_object(gathered, (w0, chains))
+    tot = g.allsum(float(n))
+    gathered = g.allgather([w0, chains.tolist()])
     if r == 0:
-        q.put((uid, t, gathered))
+        q.put((uid, t, tot, gathered, "torch" in sys.modules))
     g.close()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_two_rank_gloo_sharding_matches_single_process(world):
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_sharding_matches_single_process(world):
     total, n_iters = 5, 60
-    port = _free_port()
+    # MASTER_PORT held by another listener, as torchrun's agent store holds it
+    taken = socket.socket()
+    taken.bind(("127.0.0.1", 0))
+    taken.listen(1)
+    port = taken.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, total, n_iters, q))
              for r in range(world)]
     for p in procs:
         p.start()
-    uid, tmax, gathered = q.get(timeout=240)
+    uid, tmax, tot, gathered, torch_loaded = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert uid == b"x" * 128 and tmax == float(world)
-    got = np.concatenate([c for _, c in sorted(gathered, key=lambda x: x[0])], axis=0)
+    taken.close()
+    assert uid == b"x" * 128 and tmax == float(world) and tot == float(total)
+    assert not torch_loaded                       # the host group needs no PyTorch
+    got = np.concatenate([np.array(c).reshape(-1, n_iters, 17)
+                          for _, c in sorted(gathered, key=lambda x: x[0])], axis=0)
     ref = _oracle_chains(odist.walker_seeds(1000, 0, total), n_iters)
     np.testing.assert_array_equal(got, ref)
 

@@ -275,6 +275,13 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     assert m[0] == flat.shape[0]
     np.testing.assert_allclose(m[1:1 + s.ps], flat.sum(axis=0), rtol=1e-12)
     np.testing.assert_allclose(m[1 + s.ps:], (flat ** 2).sum(axis=0), rtol=1e-12)
+    # chain concatenation, whole and range by range (bounded receive buffer)
+    np.testing.assert_array_equal(s.allgather_chain()[0], chain)
+    parts = [s.allgather_chain(w0, 3)[0] for w0 in (0, 3)] + [s.allgather_chain(6, 2)[0]]
+    np.testing.assert_array_equal(np.concatenate(parts), chain)
+    assert s.allgather_chain(2, 4, out=False) is None
+    with pytest.raises(Exception):
+        s.allgather_chain(6, 3)                          # past the last walker
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
