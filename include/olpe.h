@@ -144,6 +144,13 @@ int olpe_last_kernel_ms(olpe_ctx *ctx, double *ms);
 /* Durations of the last n sampler launches (oldest first; n <= 64 and <= launches so
  * far): launches can be queued back to back and timed afterwards. */
 int olpe_kernel_times(olpe_ctx *ctx, int n, double *ms_out);
+/* Chunks per walker of the last sampler launch (1 = whole walkers; > 1 when the launch
+ * cut each walker's iterations into chunks to fill the resident waves).
+ * Results do not depend on it.  Build-specific: no reference counterpart. */
+int olpe_last_units(olpe_ctx *ctx, int *units);
+/* Chunk hand-offs that had to wait since the context was created: out[0] = waits,
+ * out[1] = total wave-time spent waiting (ns).  Diagnostics; build-specific. */
+int olpe_unit_stats(olpe_ctx *ctx, long long *out);
 
 /* --- chain files (apf_step2.py:342-360; 3body/apf_step2_3body.py:381-399) ---------
  * Host-only (no GPU needed).  Rows are formatted as the reference's csv.writer writes

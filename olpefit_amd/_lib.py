@@ -60,6 +60,8 @@ SIGNATURES = {
     "olpe_sync": (_i, [_P]),
     "olpe_last_kernel_ms": (_i, [_P, _pd]),
     "olpe_kernel_times": (_i, [_P, _i, _pd]),
+    "olpe_last_units": (_i, [_P, C.POINTER(C.c_int)]),
+    "olpe_unit_stats": (_i, [_P, _pll]),
     "olpe_csv_format": (_i, [_pd, _ll, _i, _i, C.c_char_p, C.c_size_t,
                              C.POINTER(C.c_size_t)]),
     "olpe_csv_write_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _i, _i, _i]),

@@ -246,6 +246,18 @@ class Sampler:
         check(self._lib.olpe_kernel_times(self._ctx, int(n), _dptr(out)))
         return out
 
+    def unit_stats(self):
+        """(waits, ns waited) of chunk hand-offs since the context was created."""
+        out = np.zeros(2, dtype=np.int64)
+        check(self._lib.olpe_unit_stats(self._ctx, out.ctypes.data_as(_lib._pll)))
+        return int(out[0]), int(out[1])
+
+    def last_units(self) -> int:
+        """Chunks per walker of the last sampler launch."""
+        v = C.c_int(0)
+        check(self._lib.olpe_last_units(self._ctx, C.byref(v)))
+        return v.value
+
     # -- multi-GPU --------------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -69,12 +69,25 @@ struct GibbsArgs {
   long long accept_min;
   double *trace;       // [W][n_iters][6] or null
   // walker queue: null = one walker per wave at blockIdx*WPB + wave; otherwise each
-  // wave takes walkers qbase.. from the counter until it passes W (persistent grid)
+  // wave takes work units qbase.. from the counter until it passes W * units
+  // (persistent grid)
   unsigned long long *queue;
   unsigned long long qbase;
+  // work units: each walker's n_iters iterations are cut into `units` consecutive
+  // chunks, unit u = chunk u / W of walker u % W (chunk-major, so a chunk's predecessor
+  // was handed out W units earlier).  Chunk k > 0 waits until uflag[w] == utag + k;
+  // the wave that ran chunk k publishes utag + k + 1 (launch_gibbs_t)
+  int units;
+  unsigned *uflag;     // [W]
+  unsigned utag;       // this launch's tag base (a multiple of 16)
+  unsigned *uerr;      // set to 1 when a hand-off wait times out (olpe_sync reports it)
+  int balance;         // progress balancing of the LDS sampler (OLPE_BALANCE)
+  int stagger;         // start offset per wave rank within a SIMD, in ~0.5 us (OLPE_STAGGER)
 };
 
 constexpr int kTraceF = 6;
+// sampler LDS header: the exp table, then 64 B of progress-balancing words
+constexpr int kSampHdr = kEtabBytes + 64;
 
 // Diagnostic build only (tools/diag_build.sh ... -DOLPE_DIAG_TIMING): per-wave cycle
 // totals of the step's sections (s_memtime), written over the trace buffer at the end.
@@ -137,8 +150,74 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
   s[0] = k.a; s[1] = k.b; s[2] = k.c;
 }
 
+// Work-unit hand-off between waves of one launch (possibly on different XCDs), the
+// publish/consume protocol of cdna_hip_programming.md Guideline 16 (R1): the producing
+// wave stores the walker's words write-through (sc1: state, counters, RNG position and
+// cached deviate, done_at; the MT key words are agent-scope stores too), drains them
+// (s_waitcnt vmcnt(0)) and sets the flag with a relaxed agent store; the consumer polls
+// the flag with relaxed agent loads and takes one agent acquire before its loads.  The
+// poll ends after 30 s of real time (100 MHz s_memrealtime) whatever happens, so the
+// grid always drains.
+// Write-through (sc1) stores of the handed-off words through global-address-space
+// pointers (never flat), so the hand-off needs no L2 write-back (release fence): the
+// guide's R1 form.  The same stores run at the end of every unit.
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ void st_wt(double *p, double v) {
+  __hip_atomic_store((gu64 *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(long long *p, long long v) {
+  __hip_atomic_store((gu64 *)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> __device__ __forceinline__ void st_wt(T *p, T v) {
+  static_assert(sizeof(T) == 4, "32-bit word");
+  unsigned u;
+  __builtin_memcpy(&u, &v, 4);
+  __hip_atomic_store((gu32 *)p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one handed-off 32-bit word read by a vector load (never the scalar cache), uniform
+template <class T> __device__ __forceinline__ T ld_uniform(const T *p) {
+  static_assert(sizeof(T) == 4, "32-bit word");
+  const unsigned u = (unsigned)__builtin_amdgcn_readfirstlane(
+      (int)__hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  T v;
+  __builtin_memcpy(&v, &u, 4);
+  return v;
+}
+__device__ __forceinline__ void unit_publish(unsigned *flag, unsigned v, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's sc1 stores have landed
+  if (lane == 0) __hip_atomic_store((gu32 *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigned *err,
+                                          unsigned long long *stats, int lane) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool waited = false;
+  for (;;) {
+    const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load((gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (v == want) break;
+    waited = true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+      __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  // hand-off statistics (olpe_unit_stats): waits and their 100 MHz ticks
+  if (waited && lane == 0) {
+    atomicAdd(stats, 1ull);
+    atomicAdd(stats + 1, __builtin_amdgcn_s_memrealtime() - t0);
+  }
+  // ONE acquire after the match: this CU's L1 may hold lines of the walker from an
+  // earlier chunk
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 #ifndef OLPE_CTRL_PRIO
-#define OLPE_CTRL_PRIO 1   // wave priority of the step's control chain (the sweep runs at 0)
+// wave priority of the step's control chain (the sweep runs at 0, or 0/1 with balancing)
+#define OLPE_CTRL_PRIO 2
 #endif
 #ifndef OLPE_GLOBAL_WAVES_PER_EU
 #define OLPE_GLOBAL_WAVES_PER_EU 3
@@ -160,7 +239,8 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
 
   // ---- LDS carve: exp table, [DE] (if staged), then one {WaveSlice, V table} per wave
   double *etab = reinterpret_cast<double *>(smem);
-  double2 *sDE = reinterpret_cast<double2 *>(smem + kEtabBytes);
+  unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
+  double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
   constexpr int TABX = drawtab_extra(NT);
   const int wstride = WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
@@ -178,8 +258,13 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     for (int k = threadIdx.x; k < npix; k += blockDim.x) sDE[k] = A.DE[k];
   }
   if (threadIdx.x < 64) etab[threadIdx.x] = c_exp2_64[threadIdx.x];
+  if (threadIdx.x == 0) s_prog[0] = 0u;
   __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
+  unsigned my_steps = 0;   // iterations this wave has started in this launch
+  // start offset: the waves of a SIMD (wave, wave + 4, wave + 8) start a fraction of a
+  // step apart so that their latency-bound control phases do not coincide
+  for (int i = 0, n = (wave >> 2) * A.stagger; i < n; ++i) __builtin_amdgcn_s_sleep(8);
 
   // Arguments used once per walker are read where they are used, through a kernarg
   // pointer the compiler cannot see through, so that they do not hold SGPRs across
@@ -202,6 +287,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     const unsigned d = v > 0x7fffffffull ? 0x7fffffffu : (unsigned)v;
     return __builtin_amdgcn_readfirstlane((int)d);
   };
+
   // chain rows: the iteration (0-based, this launch) of the next record -- count =
   // count0 + it + 1 >= burn_in and (count - burn_in) % stride == 0 -- and its row,
   // advanced by 32-bit addition (host: n_iters < 2^31); the same for every walker
@@ -216,8 +302,27 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     rec_it0 = first < niter ? (int)first : -1;
     rec_row0 = (int)(k - A.row0);
   }
-  int w = A.queue ? take() : (int)blockIdx.x * WPB + wave;
-  for (; w < K()->W; w = K()->queue ? take() : INT_MAX) {
+  int u = A.queue ? take() : (int)blockIdx.x * WPB + wave;
+  // (host: W * units < 2^31)
+  for (; u < (int)K()->W * K()->units; u = K()->queue ? take() : INT_MAX) {
+    // ---- the unit: chunk k of walker w, iterations [it_s, it_e) of this launch
+    const int units = K()->units;
+    const int Wn = (int)K()->W;
+    int w = u, k = 0, it_s = 0, it_e = niter;
+    if (units > 1) {
+      k = u / Wn;
+      w = u - k * Wn;
+      // floor(niter * k / units) in 32 bits: niter = q units + r, r k < 15 * 15
+      const int q = niter / units, r = niter - q * units;
+      it_s = q * k + (r * k) / units;
+      it_e = q * (k + 1) + (r * (k + 1)) / units;
+      // the walker's previous chunk ran on another wave: wait for its hand-off
+      if (k > 0)
+        unit_wait(K()->uflag + w, K()->utag + (unsigned)k, K()->uerr, K()->queue + 2, lane);
+    }
+#ifdef OLPE_DIAG_SPAN
+    const unsigned long long span_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // ---- walker state -> LDS slice
     if (lane < NP) {
       s_tries[lane] = K()->tries[(size_t)w * NP + lane];
@@ -236,11 +341,11 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
 
     MTWave mt;
     mt.key = K()->mt + (size_t)w * MT_N;
-    mt.pos = __builtin_amdgcn_readfirstlane(K()->mt_pos[w]);
+    mt.pos = ld_uniform(K()->mt_pos + w);
     mt.bstart = mt.pos;
     mt.bsize = 0;
     mt.batch = 0;
-    mt.has_gauss = __builtin_amdgcn_readfirstlane(K()->has_gauss[w]);
+    mt.has_gauss = ld_uniform(K()->has_gauss + w);
     mt.gauss = uniform_f64(K()->gauss[w]);
     mt.tab = drawtab;
 
@@ -252,6 +357,11 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     }
 
     int rec_it = rec_it0, rec_row = rec_row0;
+    if (rec_it0 >= 0 && it_s > rec_it0) {      // the chunk's first record
+      const int j = (it_s - rec_it0 + rstride - 1) / rstride;
+      rec_it += j * rstride;
+      rec_row += j;
+    }
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
@@ -263,7 +373,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long dt_last = __builtin_amdgcn_s_memtime();
 #endif
-    for (int it = 0; it < niter; ++it) {
+    for (int it = it_s; it < it_e; ++it) {
       // the iteration's draws: randint(0, NP) (apf_step2.py:302), the proposal's gauss()
       // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
       int r0 = 0, dice_idx = 0;
@@ -365,7 +475,23 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       // build_analytical_model + chi_squared (:314-316)
       // the step's scalar control is a latency-bound chain: it runs at raised wave
       // priority so that it is not queued behind the other waves' sweeps
-      __builtin_amdgcn_s_setprio(0);
+      if (LDS_IMG && K()->balance) {
+        // progress balancing: VALU issue among a SIMD's waves goes by age, so left alone
+        // the waves of a workgroup run at different speeds (per-wave step times spread
+        // +-25 %) and a launch ends on its slowest wave, with the SIMDs under-occupied
+        // meanwhile (one full round of walkers took 1.4x the steady-state time).  A wave
+        // that has started fewer iterations than its workgroup's mean sweeps at
+        // priority 1, the others at 0 (the control chain runs at OLPE_CTRL_PRIO above
+        // both).
+        const unsigned tot = (unsigned)__builtin_amdgcn_readfirstlane((int)s_prog[0]);
+        const bool behind = my_steps * (unsigned)WPB < tot;
+        if (lane == 0) atomicAdd(s_prog, 1u);
+        ++my_steps;
+        if (behind) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      } else {
+        __builtin_amdgcn_s_setprio(0);
+      }
       hcache.grp = grp;
       const unsigned gmask = gauss_mask<NSRC>(r);
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
@@ -411,7 +537,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
       DT_MARK(5);
 
-#ifndef OLPE_DIAG_TIMING
+#if !defined(OLPE_DIAG_TIMING) && !defined(OLPE_DIAG_SPAN)
       if (A.trace && lane == 0) {
         double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
         t[0] = (double)r;
@@ -438,21 +564,37 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     }
 #endif
 
+#ifdef OLPE_DIAG_SPAN
+    // diagnostic build only: the unit's start / end (100 MHz), HW_ID and XCC_ID in the trace
+    if (A.trace && lane < 4) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+      const double v = lane == 0 ? (double)span_t0 : lane == 1 ? (double)t1
+                     : lane == 2 ? (double)hw : (double)xcc;
+      A.trace[(size_t)w * A.n_iters * kTraceF + 4 * k + lane] = v;
+    }
+#endif
     // ---- write back (the walker index laundered: its per-lane addresses are
     // recomputed here, not kept live across the sampler loop from the loads above)
     wave_sync();
-    asm volatile("" : "+s"(w));
-    if (lane < PS) K()->state[(size_t)w * PS + lane] = st[lane];
+    // (k and w recomputed from u: one SGPR live across the loop instead of three)
+    asm volatile("" : "+s"(u));
+    k = K()->units > 1 ? u / (int)K()->W : 0;
+    w = u - k * (int)K()->W;
+    if (lane < PS) st_wt(K()->state + (size_t)w * PS + lane, st[lane]);
     if (lane < NP) {
-      K()->tries[(size_t)w * NP + lane] = s_tries[lane];
-      K()->accepts[(size_t)w * NP + lane] = s_acc[lane];
+      st_wt(K()->tries + (size_t)w * NP + lane, s_tries[lane]);
+      st_wt(K()->accepts + (size_t)w * NP + lane, s_acc[lane]);
     }
     if (lane == 0) {
-      K()->mt_pos[w] = mt.pos;
-      K()->has_gauss[w] = mt.has_gauss;
-      K()->gauss[w] = mt.gauss;
-      K()->done_at[w] = done_at;
+      st_wt(K()->mt_pos + w, mt.pos);
+      st_wt(K()->has_gauss + w, mt.has_gauss);
+      st_wt(K()->gauss + w, mt.gauss);
+      st_wt(K()->done_at + w, done_at);
     }
+    // hand the walker to the wave that takes its next chunk
+    if (k < K()->units - 1) unit_publish(K()->uflag + w, K()->utag + (unsigned)(k + 1), lane);
     wave_sync();      // the slice is reused by the wave's next walker
   }
 }
@@ -602,8 +744,47 @@ size_t wave_lds(int n, int np, bool lds_img) {
          sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt);
 }
 
+// Chunks per walker of one launch.  A launch runs W walker chains of n_iters
+// iterations on `slots` resident waves.  With whole walkers as the queue's units, W
+// just above a multiple of the slots leaves most slots idle for the last walker's
+// whole launch (configs[1]: 4,096 walkers on 3,072 slots take two walker-times instead
+// of 1 1/3).  Cutting every chain into P consecutive chunks (chunk-major queue order,
+// a chunk handed between waves through HBM, unit_wait/unit_publish) lets the queue fill
+// the slots; a chain still runs its chunks in order, so a launch takes at least one
+// chain's time.  Modelled time, in iterations, with s0 iterations' worth of per-chunk
+// setup (state and counter loads, cache setup, the hand-off):
+//   T(P) = max(ceil(W P / slots) (n_iters / P + s0), n_iters + P s0)
+// P > 1 is taken only when it beats P = 1 by more than 3 %.  override > 0 forces P
+// (OLPE_UNITS, tests and A/B).
+int choose_units(long long W, long long slots, long long n_iters, int override_p) {
+  const int pmax = 15;                 // the chunk index lives in 4 bits of the tag
+  auto ok = [&](int p) { return p <= pmax && p <= n_iters && W * p < 0x7fffffffLL; };
+  if (override_p > 0) {
+    int p = override_p;
+    while (p > 1 && !ok(p)) --p;
+    return p;
+  }
+  if (n_iters < 16 || slots <= 0 || W <= 0) return 1;
+  const double s0 = 2.0;
+  auto T = [&](int p) {
+    const double rounds = (double)((W * p + slots - 1) / slots);
+    return std::max(rounds * ((double)n_iters / p + s0), (double)n_iters + p * s0);
+  };
+  int best = 1;
+  double tb = T(1);
+  for (int p = 2; p <= 8; ++p) {
+    if (!ok(p) || n_iters / p < 8) break;
+    const double t = T(p);
+    if (t < tb) {
+      tb = t;
+      best = p;
+    }
+  }
+  return tb < 0.97 * T(1) ? best : 1;
+}
+
 size_t lds_bytes(const olpe_ctx *c, int wpb) {
-  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img) + kEtabBytes;
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   return b;
 }
@@ -625,21 +806,38 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   GibbsArgs q = a;
   q.queue = nullptr;
   q.qbase = 0;
-  if (LDS && c->queue_on && c->d_queue) {
-    // persistent grid: as many workgroups as fit on the device at once, the walkers
-    // handed out by the queue
-    int per_cu = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
-    const unsigned resident = (unsigned)std::max(1, per_cu) * (unsigned)c->n_cu;
+  q.units = 1;
+  q.uflag = c->d_uflag;
+  q.utag = 0;
+  q.uerr = reinterpret_cast<unsigned *>(c->d_queue + 1);
+  q.balance = c->balance;
+  q.stagger = c->stagger;
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
+  const unsigned resident = (unsigned)std::max(1, per_cu) * (unsigned)c->n_cu;
+  const int units = c->queue_on && c->d_queue && c->d_uflag
+                        ? choose_units(a.W, (long long)resident * WPB, a.n_iters, c->units_override)
+                        : 1;
+  // the LDS sampler always runs persistent; the L2-resident one only when it cuts the
+  // walkers into chunks (with whole walkers the hardware's workgroup dispatch is as good)
+  if (c->queue_on && c->d_queue && (LDS || units > 1)) {
+    // persistent grid: as many workgroups as fit on the device at once, the work
+    // units handed out by the queue
     if (blocks > resident) blocks = resident;
     q.queue = c->d_queue;
     q.qbase = c->qbase;
+    q.units = units;
+    c->utag += 16;
+    q.utag = c->utag;
   }
+  c->last_units = q.units;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
-  // the launch takes W + (its waves) values off the counter: the next launch's base
-  // (advanced only once the launch is in the stream)
-  if (q.queue) c->qbase += (unsigned long long)a.W + (unsigned long long)blocks * WPB;
+  // the launch takes W * units + (its waves) values off the counter: the next
+  // launch's base (advanced only once the launch is in the stream)
+  if (q.queue)
+    c->qbase += (unsigned long long)a.W * (unsigned long long)q.units +
+                (unsigned long long)blocks * WPB;
   return OLPE_OK;
 }
 
@@ -684,6 +882,8 @@ int ensure_ensemble(olpe_ctx *c, int W) {
   if ((rc = dev_alloc(&c->d_gauss, (size_t)W))) return rc;
   if ((rc = dev_alloc(&c->d_hasg, (size_t)W))) return rc;
   if ((rc = dev_alloc(&c->d_done, (size_t)W))) return rc;
+  if ((rc = dev_alloc(&c->d_uflag, (size_t)W))) return rc;
+  HIPCHK(hipMemsetAsync(c->d_uflag, 0, (size_t)W * sizeof(unsigned), c->stream));
   HIPCHK(hipMemsetAsync(c->d_state, 0, (size_t)W * c->ps * sizeof(double), c->stream));
   HIPCHK(hipMemsetAsync(c->d_tries, 0, (size_t)W * c->np * sizeof(uint32_t), c->stream));
   HIPCHK(hipMemsetAsync(c->d_acc, 0, (size_t)W * c->np * sizeof(uint32_t), c->stream));
@@ -748,7 +948,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   const size_t npix_ = (size_t)nx * nx;
   const bool lds_img = npix_ * sizeof(double2) +
                            ((nx == 64 || nx == 32) ? 12 : 16) * wave_lds(nx, np_, true) +
-                           kEtabBytes <= 160 * 1024;
+                           kSampHdr <= 160 * 1024;
   int wpb = 0;
   if (const char *e = getenv("OLPE_WPB")) {                  // tuning experiments
     // only the 64x64 LDS sampler has a choice (8 / 12 / 16 waves); its layout must fit
@@ -756,7 +956,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     wpb = atoi(e);
     if (wpb != 8 && wpb != 12 && wpb != 16)
       return set_err(OLPE_EINVAL, "OLPE_WPB=%s: must be 8, 12 or 16", e);
-    const size_t b = (size_t)wpb * wave_lds(nx, np_, true) + kEtabBytes + npix_ * sizeof(double2);
+    const size_t b = (size_t)wpb * wave_lds(nx, np_, true) + kSampHdr + npix_ * sizeof(double2);
     if (lds_img && nx == 64 && b > 160 * 1024)
       return set_err(OLPE_EINVAL, "OLPE_WPB=%d needs %zu bytes of LDS at %dx%d (%d sources) > 163840",
                      wpb, b, nx, nx, nsrc);
@@ -805,17 +1005,29 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     for (auto &ev : pair)
       if (hipEventCreate(&ev) != hipSuccess) ev = nullptr;
   if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
-      (rc = dev_alloc(&c->d_queue, 1))) {
+      (rc = dev_alloc(&c->d_queue, 4))) {
     olpe_destroy(c);
     return rc;
   }
-  if (hipMemset(c->d_queue, 0, sizeof(unsigned long long)) != hipSuccess ||
+  // [0] the queue counter, [1] the hand-off error word, [2..3] hand-off statistics
+  // (unit_wait)
+  if (hipMemset(c->d_queue, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
       hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
           hipSuccess || c->n_cu <= 0) {
     olpe_destroy(c);
     return set_err(OLPE_EHIP, "walker queue setup failed");
   }
   if (const char *e = getenv("OLPE_NO_QUEUE")) c->queue_on = atoi(e) == 0;  // A/B only
+  if (const char *e = getenv("OLPE_UNITS")) {                                // tests, A/B
+    const int p = atoi(e);
+    if (p < 0 || p > 15) {
+      olpe_destroy(c);
+      return set_err(OLPE_EINVAL, "OLPE_UNITS=%s: must be 0 (automatic) .. 15", e);
+    }
+    c->units_override = p;
+  }
+  if (const char *e = getenv("OLPE_BALANCE")) c->balance = atoi(e) != 0;   // A/B
+  if (const char *e = getenv("OLPE_STAGGER")) c->stagger = std::max(0, std::min(1000, atoi(e)));
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 == hipSuccess)
     e2 = hipMemcpy(c->d_DW, hDW.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
@@ -835,7 +1047,7 @@ void olpe_destroy(olpe_ctx *c) {
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue,
-                  c->d_gather};
+                  c->d_gather, c->d_uflag};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &pair : c->ev)
@@ -916,6 +1128,16 @@ int olpe_seed(olpe_ctx *c, const uint32_t *seeds, int W) {
   return OLPE_OK;
 }
 
+// the hand-off error word of the work-unit queue (unit_wait): a wait that timed out
+// means a chunk may have run from a stale state -- reported, never silently used
+static int check_units(olpe_ctx *c) {
+  if (!c->d_queue || c->last_units <= 1) return OLPE_OK;
+  unsigned long long e = 0;
+  HIPCHK(hipMemcpy(&e, c->d_queue + 1, sizeof(e), hipMemcpyDeviceToHost));
+  if (e) return set_err(OLPE_EHIP, "sampler chunk hand-off timed out (30 s): results invalid");
+  return OLPE_OK;
+}
+
 static int counters_to_dev(olpe_ctx *c, const double *h, uint32_t *d) {
   const size_t m = (size_t)c->W * c->np;
   std::vector<uint32_t> t(m, 0u);
@@ -964,7 +1186,7 @@ int olpe_state_get(olpe_ctx *c, double *state, double *tries, double *accepts) {
   int rc;
   if (tries && (rc = counters_to_host(c, c->d_tries, tries))) return rc;
   if (accepts && (rc = counters_to_host(c, c->d_acc, accepts))) return rc;
-  return OLPE_OK;
+  return check_units(c);
 }
 
 int olpe_run(olpe_ctx *c, long long n_iters, long long burn_in, int record_stride,
@@ -1176,6 +1398,23 @@ int olpe_sync(olpe_ctx *c) {
   if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return check_units(c);
+}
+
+int olpe_unit_stats(olpe_ctx *c, long long *out) {
+  if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned long long v[2] = {0, 0};
+  HIPCHK(hipMemcpy(v, c->d_queue + 2, sizeof(v), hipMemcpyDeviceToHost));
+  out[0] = (long long)v[0];
+  out[1] = (long long)(v[1] * 10);       // 100 MHz ticks -> ns
+  return OLPE_OK;
+}
+
+int olpe_last_units(olpe_ctx *c, int *units) {
+  if (!c || !units) return set_err(OLPE_EINVAL, "NULL argument");
+  *units = c->last_units;
   return OLPE_OK;
 }
 

@@ -106,12 +106,15 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 // The key stays in HBM (one 2,496-B row per walker); it is only touched by a refill
 // of the 64-word batch (every 64 draws) and by the twist (every 624), through
 // agent-scope atomics so that a load sees this wave's earlier stores.
+// (global address space: sc1 global loads/stores, not flat -- the key is also handed
+// between waves with a walker's chunks, olpe.hip unit_wait)
 __device__ __forceinline__ uint32_t key_ld(const uint32_t *k, int i) {
-  return __hip_atomic_load(const_cast<uint32_t *>(k) + i, __ATOMIC_RELAXED,
+  return __hip_atomic_load((__attribute__((address_space(1))) uint32_t *)(k + i), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void key_st(uint32_t *k, int i, uint32_t v) {
-  __hip_atomic_store(k + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)(k + i), v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t lane_from(uint32_t v, int src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((src_lane & 63) << 2, (int)v);

@@ -49,6 +49,14 @@ struct olpe_ctx {
   unsigned long long qbase = 0;
   bool queue_on = true;
   int n_cu = 0;
+  // work units (choose_units): walkers cut into chunks handed between waves through
+  // uflag[W]; utag = the last launch's tag base (+16 per launch)
+  unsigned *d_uflag = nullptr;
+  unsigned utag = 0;
+  int units_override = 0;   // OLPE_UNITS
+  int last_units = 1;       // chunks per walker of the last launch (olpe_last_units)
+  int balance = 0;          // progress balancing (OLPE_BALANCE)
+  int stagger = 0;          // wave start offsets (OLPE_STAGGER)
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;

@@ -396,6 +396,121 @@ def test_walker_queue_equals_static_mapping(golden, lib_loaded, monkeypatch):
     assert np.all(sa[1].sum(axis=1) == 100)
 
 
+def _run_units(g, mode, W, seeds, units, no_queue="0", monkeypatch=None, trace=False,
+               accept_min=0):
+    monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
+    monkeypatch.setenv("OLPE_UNITS", str(units))
+    s = make_sampler(g, mode)
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    s.enable_trace(trace)
+    # launches whose chunk bounds, record rows and burn-in fall at odd places
+    chains, traces, used = [], [], []
+    for n, burn, stride in ((31, 7, 5), (45, 0, 4), (17, 60, 3)):
+        chains.append(s.run(n, burn_in=burn, record_stride=stride, accept_min=accept_min))
+        used.append(s.last_units())
+        if trace:
+            traces.append(s.trace(n))
+    out = (chains, traces, s.get_state(), s.rng_state(), s.done_at(), used)
+    s.close()
+    return out
+
+
+def _assert_same_run(a, b):
+    for x, y in zip(a[0], b[0]):
+        if x is None or y is None:
+            assert x is None and y is None
+        else:
+            np.testing.assert_array_equal(x, y)
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a[2] + a[3], b[2] + b[3]):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a[4], b[4])
+
+
+@pytest.mark.parametrize("units", [0, 2, 3, 7])
+def test_work_units_equal_whole_walkers(golden, lib_loaded, monkeypatch, units):
+    """Walkers cut into chunks handed between waves (OLPE_UNITS): 4,099
+    walkers (more than the 3,072 resident waves) over three launches give every
+    chain row, trace entry, final state, counter, RNG state and done_at bit for bit
+    equal to the static one-walker-per-wave mapping.  units = 0 is the automatic
+    choice: 2 chunks for each of these launches (4,099 walkers fill 1 1/3 rounds of
+    whole walkers, 2 2/3 of half walkers)."""
+    g = golden("c64")
+    W = 4099
+    seeds = 9000 + np.arange(W)
+    ref = _run_units(g, "fast", W, seeds, 0, "1", monkeypatch, trace=True, accept_min=4)
+    got = _run_units(g, "fast", W, seeds, units, "0", monkeypatch, trace=True, accept_min=4)
+    _assert_same_run(got, ref)
+    assert got[5] == [units or 2] * 3
+    assert ref[5] == [1, 1, 1]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_work_units_few_walkers_spin(golden, lib_loaded, monkeypatch, mode):
+    """13 walkers cut into 15 chunks: all 195 units are taken at once, so 182 waves
+    wait on a hand-off -- every chunk's predecessor runs on another wave, often on
+    another XCD.  Results equal whole walkers and the oracle."""
+    g = golden("c32")
+    W = 13
+    seeds = 500 + np.arange(W)
+    ref = _run_units(g, mode, W, seeds, 0, "1", monkeypatch)
+    got = _run_units(g, mode, W, seeds, 15, "0", monkeypatch)
+    _assert_same_run(got, ref)
+    assert got[5] == [15, 15, 15]
+
+
+def test_work_units_l2_sampler(lib_loaded, monkeypatch):
+    """The 128x128 (L2-resident) sampler runs persistent only when it cuts walkers
+    into chunks: chunks of 3 and of 5 equal its static mapping bit for bit."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    n, nsrc, W = 128, 3, 3100
+    img, _ = synth.make_image(n, nsrc, 0)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    out = []
+    for no_queue, units in (("1", 0), ("0", 3), ("0", 5)):
+        monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
+        monkeypatch.setenv("OLPE_UNITS", str(units))
+        s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+        p0[-1] = s.chi_squared(p0)
+        s.seed(2000 + np.arange(W))
+        s.set_state(np.tile(p0, (W, 1)))
+        c = s.run(40, burn_in=0, record_stride=3)
+        out.append((c, s.get_state(), s.rng_state(), s.last_units()))
+        s.close()
+    assert [o[3] for o in out] == [1, 3, 5]
+    for o in out[1:]:
+        np.testing.assert_array_equal(o[0], out[0][0])
+        for x, y in zip(o[1] + o[2], out[0][1] + out[0][2]):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_work_units_automatic_choice(lib_loaded, monkeypatch):
+    """configs[1]'s shape (4,096 walkers, 64x64, 100 iterations) is cut into 3 chunks
+    per walker (4 full rounds of the 3,072 resident waves instead of 1 1/3); configs[2]
+    (65,536) keeps whole walkers."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    monkeypatch.delenv("OLPE_UNITS", raising=False)
+    monkeypatch.delenv("OLPE_NO_QUEUE", raising=False)
+    img, _ = synth.make_image(64, 2, 0)
+    p0 = initial_parameters(img, synth.guess_values(64, 2), 2)
+    got = {}
+    for W in (4096, 65536):
+        s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+        p0[-1] = s.chi_squared(p0)
+        s.seed(1000 + np.arange(W))
+        s.set_state(np.tile(p0, (W, 1)))
+        s.run(100, burn_in=0, record_stride=10, read_chain=False)
+        got[W] = s.last_units()
+        s.close()
+    assert got == {4096: 3, 65536: 1}, got
+
+
 @pytest.mark.parametrize("n,nsrc,mode", [(40, 2, "fast"), (40, 2, "exact"), (48, 3, "fast"),
                                          (80, 2, "fast"), (96, 3, "fast"), (128, 2, "fast"),
                                          (24, 2, "fast"), (32, 3, "fast"), (32, 3, "exact"),

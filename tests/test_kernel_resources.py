@@ -5,11 +5,17 @@ The 64x64 two-source sampler runs 12 waves per workgroup (3 per SIMD), which cap
 wave at 168 VGPRs; DESIGN.md §3 relies on it having no scratch at all (spilled column
 terms cost the 16-wave variant 0.25 GB of extra HBM writes per launch).  A change that
 makes the FAST or EXACT bench kernel spill fails here before it reaches a GPU.
+
+"No scratch" means no scratch memory instruction in the kernel and no spilled VGPR:
+since the work-unit loop the compiler reserves a 36-B private segment
+frame for these kernels that no instruction touches (its SGPR spills live in VGPR
+lanes), so the reserved size alone is not the criterion.
 """
 import os
 import re
 import shutil
 import subprocess
+import tempfile
 
 import pytest
 
@@ -27,7 +33,17 @@ def usage():
     cmd = [HIPCC, *flags, "--cuda-device-only", "-c", "-o", os.devnull,
            os.path.join(REPO, "olpefit_amd", "csrc", "olpe.hip"),
            "-Rpass-analysis=kernel-resource-usage"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900).stderr
+    with tempfile.TemporaryDirectory() as td:
+        asm = os.path.join(td, "olpe.s")
+        cmd[cmd.index("-c")] = "-S"
+        cmd[cmd.index(os.devnull)] = asm
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=900).stderr
+        text = open(asm).read()
+    # scratch memory instructions per kernel body
+    bodies = {}
+    for m in re.finditer(r"^(_Z\S*olpe_gibbs_kernel\S*):[^\n]*\n(.*?)^\.Lfunc_end", text, re.M | re.S):
+        bodies[m.group(1)] = len(re.findall(r"^\s+(scratch_|buffer_(load|store)\S*.*off(en|set)?.*s\[0:3\])",
+                                            m.group(2), re.M))
     res = {}
     name = None
     for line in out.splitlines():
@@ -39,6 +55,8 @@ def usage():
         m = re.search(r"remark:\s+(VGPRs|ScratchSize \[bytes/lane\]|VGPRs Spill): (\d+)", line)
         if m and name:
             res[name][m.group(1)] = int(m.group(2))
+    for name, v in res.items():
+        v["scratch_insts"] = bodies.get(name, -1)
     return res
 
 
@@ -52,7 +70,7 @@ def _kernel(usage, nsrc, nt, lds, wpb, fast):
 @pytest.mark.parametrize("fast", [True, False])
 def test_bench_sampler_has_no_scratch(usage, fast):
     k = _kernel(usage, 2, 64, True, 12, fast)
-    assert k["ScratchSize [bytes/lane]"] == 0, k
+    assert k["scratch_insts"] == 0 and k["VGPRs Spill"] == 0, k
     assert k["VGPRs"] <= 168, k
 
 
@@ -61,4 +79,4 @@ def test_other_bench_configs_have_no_scratch(usage):
     # and the 3-source 64x64 LDS sampler
     for args in [(3, 128, False, 4, True), (3, 64, True, 12, True)]:
         k = _kernel(usage, *args)
-        assert k["ScratchSize [bytes/lane]"] == 0, (args, k)
+        assert k["scratch_insts"] == 0 and k["VGPRs Spill"] == 0, (args, k)

@@ -18,4 +18,6 @@ tools/gpu_steps.sh \
   "prof_c4:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_c4_fast -o run --output-format csv -- $B --config 4" \
   "pmc_fetch_c4:300:rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${tag}_fetch_c4_fast -o run --output-format csv -- $B --config 4" \
   "pmc_write_c4:300:rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${tag}_write_c4_fast -o run --output-format csv -- $B --config 4" \
-  "bench_c4:300:python bench.py --config 4"
+  "bench_c4:300:python bench.py --config 4" \
+  "prof_c1:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_c1_fast -o run --output-format csv -- $B --config 1" \
+  "bench_c1:300:python bench.py --config 1"
