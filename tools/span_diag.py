@@ -28,11 +28,13 @@ def main():
     s.seed(1000 + np.arange(W))
     s.set_state(np.tile(p0, (W, 1)))
     s.enable_trace(True)
-    for _ in range(3):
-        s.run(iters, burn_in=0, record_stride=10, read_chain=False)
+    # back to back, as bench.py queues them (no idle gap before the traced launch)
+    for _ in range(int(os.environ.get("SPAN_LAUNCHES", "6"))):
+        s.run_async(iters, burn_in=0, record_stride=10)
+    s.sync()
     km = s.kernel_times(1)[0]
     P = s.last_units()
-    tr = s.trace(iters).reshape(W, -1)[:, :4 * P].reshape(W, P, 4)
+    tr = s.trace(iters).reshape(W, -1)[:, :5 * P].reshape(W, P, 5)
     t0, t1 = tr[..., 0] * 10e-6, tr[..., 1] * 10e-6          # ms
     base = t0.min()
     t0, t1 = t0 - base, t1 - base
@@ -44,11 +46,13 @@ def main():
     se = (hw >> 13) & 7
     slot = ((xcc * 8 + se) * 2 + sh) * 16 + cu
     dur = t1 - t0
+    clk = tr[..., 4] / (dur * 1e-3) / 1e9                  # s_memtime ticks per second (GHz)
     q = lambda a: " ".join(f"{np.percentile(a, p):.3f}" for p in (0, 10, 50, 90, 100))
     print(f"W={W} iters={iters} units={P} kernel_ms={km:.3f}  (percentiles 0/10/50/90/100)")
     print(f"  unit start ms: {q(t0)}")
     print(f"  unit end   ms: {q(t1)}")
     print(f"  unit dur   ms: {q(dur)}")
+    print(f"  s_memtime rate GHz: {q(clk)}")
     print(f"  last end - kernel: {t1.max():.3f} of {km:.3f}")
     # spread of end times among the waves of one SIMD (last unit of each walker)
     key = slot * 4 + simd
