@@ -322,6 +322,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     }
 #ifdef OLPE_DIAG_SPAN
     const unsigned long long span_t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long span_c0 = __builtin_amdgcn_s_memtime();
 #endif
     // ---- walker state -> LDS slice
     if (lane < NP) {
@@ -365,6 +366,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
+    GuardCache gcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
     ccache.colc = colc;
@@ -494,8 +496,9 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       }
       hcache.grp = grp;
       const unsigned gmask = gauss_mask<NSRC>(r);
+      gcache.same = gmask == 0 && grp == 0;
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
-                                                       &hcache, &ccache, gmask);
+                                                       &hcache, &ccache, gmask, &gcache);
       __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
       DT_MARK(3);
       const double chi = wave_sum(part);
@@ -515,6 +518,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
         acc = __builtin_amdgcn_readfirstlane(dice < exp(la) ? 1 : 0) != 0;
       }
       hcache.after(acc);
+      gcache.after(acc);
       if constexpr (FAST && NT != 0 && NT <= 64) {
 #ifndef OLPE_DIAG_NO_REFRESH
         if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
@@ -566,13 +570,14 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
 
 #ifdef OLPE_DIAG_SPAN
     // diagnostic build only: the unit's start / end (100 MHz), HW_ID and XCC_ID in the trace
-    if (A.trace && lane < 4) {
+    if (A.trace && lane < 5) {
       const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
       const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
       const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
       const double v = lane == 0 ? (double)span_t0 : lane == 1 ? (double)t1
-                     : lane == 2 ? (double)hw : (double)xcc;
-      A.trace[(size_t)w * A.n_iters * kTraceF + 4 * k + lane] = v;
+                     : lane == 2 ? (double)hw : lane == 3 ? (double)xcc : (double)(c1 - span_c0);
+      A.trace[(size_t)w * A.n_iters * kTraceF + 5 * k + lane] = v;
     }
 #endif
     // ---- write back (the walker index laundered: its per-lane addresses are

@@ -66,16 +66,31 @@ __device__ __forceinline__ double dpp_f64(double v) {
   return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
 }
 
+// one DPP move of a double without an "old" operand: the lanes the row mask leaves
+// out keep whatever the register held (no zeroing moves); only for reductions whose
+// result is read from lanes every stage wrote
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64_any(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
 // Wave-wide sum with DPP (no LDS round trips): quad_perm [1,0,3,2] / [2,3,0,1],
-// row_half_mirror, row_mirror, row_bcast:15 (rows 1,3), row_bcast:31 (rows 2,3);
-// lane 63 ends with the total, broadcast with readlane.
+// row_half_mirror, row_mirror (every lane of a row then holds the row's sum),
+// row_bcast:15 (rows 1,3 add lane 15 / 47 of the row before), row_bcast:31 (rows 2,3
+// add lane 31); lane 63 ends with the total, broadcast with readlane.  Only lanes
+// 31 and 63 of the last two stages are read, and both lie in the rows those stages
+// write, so the lanes the row masks leave out may hold anything: the moves need no
+// zeroed "old" operand (2 VALU per stage fewer).
 __device__ __forceinline__ double wave_sum(double v) {
-  v += dpp_f64<0xB1, 0xf>(v);
-  v += dpp_f64<0x4E, 0xf>(v);
-  v += dpp_f64<0x141, 0xf>(v);
-  v += dpp_f64<0x140, 0xf>(v);
-  v += dpp_f64<0x142, 0xa>(v);
-  v += dpp_f64<0x143, 0xc>(v);
+  v += dpp_f64_any<0xB1, 0xf>(v);
+  v += dpp_f64_any<0x4E, 0xf>(v);
+  v += dpp_f64_any<0x141, 0xf>(v);
+  v += dpp_f64_any<0x140, 0xf>(v);
+  v += dpp_f64_any<0x142, 0xa>(v);
+  v += dpp_f64_any<0x143, 0xc>(v);
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
@@ -899,6 +914,24 @@ __device__ __forceinline__ void build_htab(const ModelDesc<NSRC> &m, double *tab
 // Per-walker cache of the FAST3 tables in the two halves of the wave's vtab area: slot
 // `cur` holds the tables of the current state when `valid`; a shape proposal builds its
 // tables in the other slot (`flip` = that slot holds the proposal's tables).
+// FAST3 guard result of the current state (sampler kernels): a draw that moves no
+// Gaussian and no shape (amplitudes, ratio, offset: gauss_mask 0, grp 0 -- 4 of the
+// 16 draws of the 2-source model) leaves every guard input but the amplitudes
+// unchanged, and the guard's only amplitude test (finite) cannot change the step's
+// outcome: a non-finite amplitude makes chi^2 NaN, which rejects, in every sweep.
+// So such a draw reuses the current state's result.
+struct GuardCache {
+  bool same = false;    // this step's draw leaves the guard inputs unchanged
+  bool valid = false;   // cur holds the current state's guard
+  bool cur = false, prop = false;
+  __device__ __forceinline__ void after(bool accepted) {
+    if (same || accepted) {
+      cur = prop;
+      valid = true;
+    }
+  }
+};
+
 struct HCache {
   int cur = 0;
   bool valid = false;
@@ -1294,7 +1327,8 @@ template <int NSRC, int NT, bool WRITE, bool FAST, bool WIDE = false>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane,
                                         const double *etab, HCache *hc = nullptr,
-                                        ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0) {
+                                        ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0,
+                                        GuardCache *gc = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
@@ -1331,7 +1365,9 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
         ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane, fails);
       }
     } else {
-      ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+      if (gc && gc->same && gc->valid) ok3 = gc->cur;
+      else ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
+      if (gc) gc->prop = ok3;
     }
 #endif
     asm volatile("" ::: "memory");
