@@ -1248,9 +1248,30 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         }
       } else {
         double2 hc[BLK], hn[BLK];
+        // cutout row r of this lane's column.  The L2-resident cutout (n > 64) is read
+        // through a buffer descriptor: the lane's column offset is a fixed VGPR and the
+        // row offset a wave-uniform SGPR (SALU adds), where 64-bit flat addresses
+        // took two VALU adds per row (~250 VALU per 128x128 walker-step)
+        [[maybe_unused]] __amdgpu_buffer_rsrc_t rsrc;
+        [[maybe_unused]] int voff = 0;
+        if constexpr (NT > 64) {
+          rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(DW), (short)0,
+                                                   NT * NT * 16, 0x00020000);
+          voff = (cw.grp * n + jj) * 16;
+        }
+        auto img = [&](int r) -> double2 {
+          if constexpr (NT > 64) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, r * rstep * 16, 0);
+            double2 d;
+            __builtin_memcpy(&d, &v, 16);
+            return d;
+          } else {
+            return p[r * rstep];
+          }
+        };
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
-          cur[k] = p[k * rstep];
+          cur[k] = img(k);
           hc[k] = hr[k];
       }
       // n >= 64 (S = 1): rows = n is a compile-time count and the row loop is unrolled
@@ -1263,7 +1284,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         const int hb = more ? b0 + BLK : b0;
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
-          nxt[k] = pn[k * rstep];
+          nxt[k] = NT > 64 ? img(hb + k) : pn[k * rstep];
           hn[k] = hr[hb + k];
         }
 #pragma unroll

@@ -370,6 +370,40 @@ def test_bench_3source_128_matches_oracle(lib_loaded):
         assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
 
 
+def test_configs4_full_shard_matches_oracle(lib_loaded, monkeypatch):
+    """configs[4]'s per-GPU shard at full size: 16,384 walkers (131,072 over 8 GPUs) on
+    the 3-source 128x128 synthetic cutout, FAST, the bench's seeds, start and launch
+    shape (100 iterations, stride 10; the automatic choice cuts each walker into 3
+    chunks handed between waves).  Two launches; walkers spread over the shard
+    (first, last, chunk-boundary neighbours) equal the oracle run of their seeds, every
+    chain is finite and every walker tried 200 parameters."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    monkeypatch.delenv("OLPE_UNITS", raising=False)
+    monkeypatch.delenv("OLPE_NO_QUEUE", raising=False)
+    n, nsrc, W, n_it = 128, 3, 16384, 100
+    img, _ = synth.make_image(n, nsrc, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    p0[-1] = s.chi_squared(p0)
+    seeds = 1000 + np.arange(W)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (W, 1)))
+    c1 = s.run(n_it, burn_in=0, record_stride=10)
+    assert s.last_units() == 3
+    c2 = s.run(n_it, burn_in=0, record_stride=10)
+    chain = np.concatenate([c1, c2], axis=1)
+    assert chain.shape == (W, 2 * n_it // 10, s.ps) and np.all(np.isfinite(chain))
+    for w in (0, 5461, 5462, 10923, W - 1):
+        ref, _ = ora.Walker(dm, err, p0, int(seeds[w]), nsrc=nsrc).run(2 * n_it, record_stride=10)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9)
+    st, tries, acc = s.get_state()
+    assert np.all(tries.sum(axis=1) == 2 * n_it) and np.all(acc <= tries)
+    s.close()
+
+
 def test_walker_queue_equals_static_mapping(golden, lib_loaded, monkeypatch):
     """The persistent sampler hands walkers out from a device counter (DESIGN.md §3);
     with more walkers than resident waves (4,099 > 256 CUs x 16) some waves run two.
