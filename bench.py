@@ -250,6 +250,7 @@ def main():
         return allmax(t1 - t0), float(np.mean(kms))
 
     elapsed, kernel_ms = measure(args.mode, args.steps, args.warmup)
+    units = s.last_units()          # chunks per walker of the timed launches
     st, tries, accs = s.get_state()
     acceptance = float(accs.sum() / max(1.0, tries.sum()))
     alt = None
@@ -372,6 +373,7 @@ def main():
         "config": {"workload": CONFIG_NAMES[args.config], "walkers_per_gpu": wpg,
                    "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                    "chain_stride": args.stride, "eval": args.mode,
+                   "chunks_per_walker": units,
                    "parallelism": f"walker-sharded x{world}"},
         "roofline": roofline(args.mode, kernel_ms),
         "acceptance": acceptance,
