@@ -114,10 +114,11 @@ template <int NP> struct WaveSlice {
   static constexpr int U32 = 2 * NP;                         // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
   static constexpr int NSRC = NP == 16 ? 2 : 3;
-  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3]
+  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3] | proposal[PS]
   static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
   static constexpr int OPT = PS + 12, OPC = PS + 15;
-  static constexpr int F64 = PS + 18;
+  static constexpr int OPR = PS + 18;
+  static constexpr int F64 = 2 * PS + 18;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
   static constexpr int OCC = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;  // col_coef [G][3]
   static constexpr int OPE = (OCC + 2 * NSRC * 3 * 8 + 15) & ~15;
@@ -452,10 +453,14 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       // the step's model descriptor goes to LDS (the sweep loads each field where it is
       // used instead of holding 6*G doubles in registers across it), built lane-parallel:
       // lane g < G writes Gaussian g with make_model's operations, lane G the background
+      // the proposal vector, lane-parallel, so that the descriptor lanes read their
+      // fields without a per-field select against the drawn index
+      if (lane < PS) st[WS::OPR + lane] = (lane == r) ? nv : st[lane];
+      wave_sync();
       if (lane < 2 * NSRC) {
         const int s = lane >> 1;
         const bool narrow = lane & 1;
-        auto ql = [&](int k) -> double { return (k == r) ? nv : st[k]; };
+        auto ql = [&](int k) -> double { return st[WS::OPR + k]; };
         const double tot = ql(L::sa(s)) - ql(L::OFF);
         const double wide = tot * ql(L::RATIO);
         const double xc = ql(L::sx(s)), yc = ql(L::sy(s));
