@@ -841,6 +841,7 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
     q.utag = c->utag;
   }
   c->last_units = q.units;
+  if (q.units > 1) c->units_used = true;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
   // the launch takes W * units + (its waves) values off the counter: the next
@@ -1141,7 +1142,7 @@ int olpe_seed(olpe_ctx *c, const uint32_t *seeds, int W) {
 // the hand-off error word of the work-unit queue (unit_wait): a wait that timed out
 // means a chunk may have run from a stale state -- reported, never silently used
 static int check_units(olpe_ctx *c) {
-  if (!c->d_queue || c->last_units <= 1) return OLPE_OK;
+  if (!c->d_queue || !c->units_used) return OLPE_OK;   // (the word is sticky)
   unsigned long long e = 0;
   HIPCHK(hipMemcpy(&e, c->d_queue + 1, sizeof(e), hipMemcpyDeviceToHost));
   if (e) return set_err(OLPE_EHIP, "sampler chunk hand-off timed out (30 s): results invalid");
@@ -1274,7 +1275,7 @@ int olpe_chain_read(olpe_ctx *c, double *chain_out) {
   HIPCHK(hipStreamSynchronize(c->stream));
   const size_t m = (size_t)c->W * c->chain_rows * c->ps;
   if (m) HIPCHK(hipMemcpy(chain_out, c->d_chain, m * 8, hipMemcpyDeviceToHost));
-  return OLPE_OK;
+  return check_units(c);
 }
 
 int olpe_count(olpe_ctx *c, long long *count) {
@@ -1295,7 +1296,7 @@ int olpe_done_at(olpe_ctx *c, long long *done_at) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpy(done_at, c->d_done, (size_t)c->W * 8, hipMemcpyDeviceToHost));
-  return OLPE_OK;
+  return check_units(c);
 }
 
 int olpe_run_gibbs(olpe_ctx *c, double *state, double *tries, double *accepts, int W,

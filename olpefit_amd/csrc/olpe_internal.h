@@ -55,6 +55,7 @@ struct olpe_ctx {
   unsigned utag = 0;
   int units_override = 0;   // OLPE_UNITS
   int last_units = 1;       // chunks per walker of the last launch (olpe_last_units)
+  bool units_used = false;  // some launch handed chunks between waves (check_units)
   int balance = 0;          // progress balancing (OLPE_BALANCE)
   int stagger = 0;          // wave start offsets (OLPE_STAGGER)
   // RCCL communicator (olpe_comm.hip)
