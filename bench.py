@@ -35,6 +35,7 @@ import multiprocessing as mp
 import os
 import platform
 import sys
+import threading
 import time
 
 import numpy as np
@@ -161,6 +162,19 @@ def cpu_baseline(n: int, nsrc: int, total_iters: int):
                       f"cpu: {model}"}
 
 
+def _comm_timeout(rank: int, make_report, timeout: float):
+    """Watchdog of the end-of-run RCCL exchange: rank 0 prints the measurement with the
+    error, then every rank leaves (os._exit: the hung collective never returns)."""
+    print(f"[bench rank {rank}] RCCL exchange still running after {timeout:g} s: giving up",
+          file=sys.stderr)
+    if rank == 0:
+        out = make_report()
+        out["comm_error"] = f"TimeoutError: RCCL exchange did not finish within {timeout:g} s"
+        print(json.dumps(out), flush=True)
+    sys.stderr.flush()
+    os._exit(0)
+
+
 def load_json(path: str):
     try:
         with open(path) as f:
@@ -193,6 +207,9 @@ def main():
     ap.add_argument("--valu", default=os.path.join(REPO, "profiles", "valu_counts.json"))
     ap.add_argument("--gather-mib", type=float, default=1024.0,
                     help="N > 1: MiB of chain rows per rank per all-gather range")
+    ap.add_argument("--comm-timeout", type=float, default=240.0,
+                    help="N > 1: seconds the end-of-run RCCL exchange may take before rank 0 "
+                         "reports the measurement without it")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0, no RCCL "
                          "all-gather (RCCL refuses two ranks on one device)")
@@ -260,13 +277,119 @@ def main():
         e2, k2 = measure(other, alt_steps, 1)
         alt = (other, alt_steps, e2, k2)
 
+    def report(elapsed, kernel_ms, units, acceptance, comm, alt=None):
+        """rank 0's JSON line (without the CPU baseline)."""
+        total = world * wpg * args.iters * args.steps
+        value = total / elapsed
+        steps_per_launch = wpg * args.iters
+        traffic = load_json(args.traffic) or {}
+        valu = load_json(args.valu) or {}
+        from olpefit_amd.build import kernel_digest
+        digest = kernel_digest()
+        default_shape = not args.walkers and args.iters == 100 and args.stride == 10
+
+        def key(mode):
+            return mode if args.config == 2 else f"c{args.config}_{mode}"
+
+        def roofline(mode, kernel_ms):
+            """FP64-VALU roofline of the sampler kernel.  frac: executed
+            FP64 lane-ops (rocprofv3 SQ counts per walker-step, profiles/valu_counts.json)
+            x the live HIP-event walker-step rate / the FP64 vector peak."""
+            secs = kernel_ms * 1e-3
+            rate = steps_per_launch / secs                   # walker-steps/s of the kernel
+            peak = FP64_LANE_PEAK / 1e12
+            vc = valu.get(key(mode))       # per walker-step, measured at the default shape
+            out = {"bound": "fp64-valu", "peak": peak, "unit": "TFLOP/s",
+                   "kernel": "olpe_gibbs_kernel", "kernel_ms": kernel_ms,
+                   "walker_steps_per_launch": steps_per_launch}
+            if vc:
+                out.update(
+                    achieved=rate * vc["fp64_lane_ops_per_step"] / 1e12,
+                    frac=rate * vc["fp64_lane_ops_per_step"] / FP64_LANE_PEAK,
+                    frac_source="counters",
+                    fp64_lane_ops_per_walker_step=vc["fp64_lane_ops_per_step"],
+                    valu_per_walker_step=vc["valu_per_step"],
+                    valu_issue_frac=rate * vc["valu_per_step"] * 64 / FP64_LANE_PEAK,
+                    counts_stale=vc.get("kernel_digest") != digest)
+            else:                       # no counters for this shape: the model's own count
+                ops = work_per_step(n, nsrc, mode)
+                out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
+                           frac_source="operation count (model + chi^2 only; lower bound)",
+                           fp64_lane_ops_per_walker_step=ops)
+            ops = work_per_step(n, nsrc, mode)
+            out["model_chi2_frac"] = rate * ops / FP64_LANE_PEAK
+            algo = sec8d_work(n, nsrc)
+            out["equivalent_exp_form_rate"] = rate * algo / 1e12
+            out["exp_form_work_per_walker_step"] = algo
+            tb = traffic.get(key(mode), {}).get("bytes_per_launch") if default_shape else None
+            out["traffic"] = tb
+            out["hbm_gbs"] = tb / secs / 1e9 if tb else None
+            out["hbm_frac"] = tb / secs / HBM_PEAK if tb else None
+            out["note"] = (
+                "frac = executed FP64 VALU lane-ops (64 x SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 "
+                "per walker-step, FMA counted once) x HIP-event rate / 78.6e12/2; "
+                "valu_issue_frac = all VALU instructions x 64 / the same peak; model_chi2_frac = "
+                "the model + chi^2 operations alone (DESIGN.md §4); equivalent_exp_form_rate = "
+                "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 19) at this rate, in T "
+                "lane-ops/s: FAST does far fewer operations, so it is no utilisation figure; "
+                "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
+                "(profiles/pmc_traffic.json); the north star's >= 40 % HBM-read roofline does "
+                "not apply to an LDS-resident FP64-VALU-bound kernel (SURVEY.md 8(d)): hbm_frac "
+                "is reported, not targeted")
+            return out
+
+        out = {
+            "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
+            "value": value,
+            "unit": "walker-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
+            "config": {"workload": CONFIG_NAMES[args.config], "walkers_per_gpu": wpg,
+                       "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
+                       "chain_stride": args.stride, "eval": args.mode,
+                       "chunks_per_walker": units,
+                       "parallelism": f"walker-sharded x{world}"},
+            "roofline": roofline(args.mode, kernel_ms),
+            "acceptance": acceptance,
+            "allgather_ms": None,
+        }
+        out.update(comm)
+        if alt:
+            other, alt_steps, e2, k2 = alt
+            out["alt_eval"] = {"eval": other,
+                               "value": world * wpg * args.iters * alt_steps / e2,
+                               "ms_per_step": e2 / alt_steps * 1e3,
+                               "roofline": roofline(other, k2)}
+        return out
+
     # end-of-run exchange over RCCL/xGMI (SURVEY.md §8(e)), outside the timed region:
     # all-gather of the final walker states, then the chain concatenation -- the last
     # launch's chain rows of every rank, gathered range by range so that the receive
     # buffer stays under --gather-mib per rank.  An error (reported by libolpe) is
     # recorded in the JSON line instead of losing the measurement.
     comm = {}
+    watchdog = None
+
+    def watchdog_cancel():
+        if watchdog is not None:
+            watchdog.cancel()
+
     if world > 1 and not args.share_gpu:
+        # watchdog: a hung exchange (never observed; RCCL init or a collective waiting on
+        # a lost peer) must not cost the measurement -- rank 0 prints its line with the
+        # error after --comm-timeout s and every rank exits
+        watchdog = threading.Timer(args.comm_timeout, _comm_timeout,
+                                   (rank, lambda: report(elapsed, kernel_ms, units, acceptance,
+                                                         dict(comm)), args.comm_timeout))
+        watchdog.daemon = True
+        watchdog.start()
         try:
             uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
             s.comm_init(uid, world, rank)
@@ -294,98 +417,14 @@ def main():
                   file=sys.stderr)
 
     if rank != 0:
+        watchdog_cancel()
         s.close()
         group.close()
         return
 
-    total = world * wpg * args.iters * args.steps
-    value = total / elapsed
-    steps_per_launch = wpg * args.iters
-    traffic = load_json(args.traffic) or {}
-    valu = load_json(args.valu) or {}
-    from olpefit_amd.build import kernel_digest
-    digest = kernel_digest()
-    default_shape = not args.walkers and args.iters == 100 and args.stride == 10
-
-    def key(mode):
-        return mode if args.config == 2 else f"c{args.config}_{mode}"
-
-    def roofline(mode, kernel_ms):
-        """FP64-VALU roofline of the sampler kernel.  frac: executed
-        FP64 lane-ops (rocprofv3 SQ counts per walker-step, profiles/valu_counts.json)
-        x the live HIP-event walker-step rate / the FP64 vector peak."""
-        secs = kernel_ms * 1e-3
-        rate = steps_per_launch / secs                   # walker-steps/s of the kernel
-        peak = FP64_LANE_PEAK / 1e12
-        vc = valu.get(key(mode))       # per walker-step, measured at the default shape
-        out = {"bound": "fp64-valu", "peak": peak, "unit": "TFLOP/s",
-               "kernel": "olpe_gibbs_kernel", "kernel_ms": kernel_ms,
-               "walker_steps_per_launch": steps_per_launch}
-        if vc:
-            out.update(
-                achieved=rate * vc["fp64_lane_ops_per_step"] / 1e12,
-                frac=rate * vc["fp64_lane_ops_per_step"] / FP64_LANE_PEAK,
-                frac_source="counters",
-                fp64_lane_ops_per_walker_step=vc["fp64_lane_ops_per_step"],
-                valu_per_walker_step=vc["valu_per_step"],
-                valu_issue_frac=rate * vc["valu_per_step"] * 64 / FP64_LANE_PEAK,
-                counts_stale=vc.get("kernel_digest") != digest)
-        else:                       # no counters for this shape: the model's own count
-            ops = work_per_step(n, nsrc, mode)
-            out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
-                       frac_source="operation count (model + chi^2 only; lower bound)",
-                       fp64_lane_ops_per_walker_step=ops)
-        ops = work_per_step(n, nsrc, mode)
-        out["model_chi2_frac"] = rate * ops / FP64_LANE_PEAK
-        algo = sec8d_work(n, nsrc)
-        out["equivalent_exp_form_rate"] = rate * algo / 1e12
-        out["exp_form_work_per_walker_step"] = algo
-        tb = traffic.get(key(mode), {}).get("bytes_per_launch") if default_shape else None
-        out["traffic"] = tb
-        out["hbm_gbs"] = tb / secs / 1e9 if tb else None
-        out["hbm_frac"] = tb / secs / HBM_PEAK if tb else None
-        out["note"] = (
-            "frac = executed FP64 VALU lane-ops (64 x SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 "
-            "per walker-step, FMA counted once) x HIP-event rate / 78.6e12/2; "
-            "valu_issue_frac = all VALU instructions x 64 / the same peak; model_chi2_frac = "
-            "the model + chi^2 operations alone (DESIGN.md §4); equivalent_exp_form_rate = "
-            "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 19) at this rate, in T "
-            "lane-ops/s: FAST does far fewer operations, so it is no utilisation figure; "
-            "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
-            "(profiles/pmc_traffic.json); the north star's >= 40 % HBM-read roofline does "
-            "not apply to an LDS-resident FP64-VALU-bound kernel (SURVEY.md 8(d)): hbm_frac "
-            "is reported, not targeted")
-        return out
-
-    out = {
-        "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
-        "value": value,
-        "unit": "walker-steps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
-        "config": {"workload": CONFIG_NAMES[args.config], "walkers_per_gpu": wpg,
-                   "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
-                   "chain_stride": args.stride, "eval": args.mode,
-                   "chunks_per_walker": units,
-                   "parallelism": f"walker-sharded x{world}"},
-        "roofline": roofline(args.mode, kernel_ms),
-        "acceptance": acceptance,
-        "allgather_ms": None,
-    }
-    out.update(comm)
-    if alt:
-        other, alt_steps, e2, k2 = alt
-        out["alt_eval"] = {"eval": other,
-                           "value": world * wpg * args.iters * alt_steps / e2,
-                           "ms_per_step": e2 / alt_steps * 1e3,
-                           "roofline": roofline(other, k2)}
+    watchdog_cancel()
+    out = report(elapsed, kernel_ms, units, acceptance, comm, alt)
+    value = out["value"]
     if not args.no_cpu_baseline and world == 1:
         cpu_steps = args.cpu_steps or max(4000, 96000 * 64 * 64 // (n * n))
         out["cpu_baseline"] = cpu_baseline(n, nsrc, cpu_steps)

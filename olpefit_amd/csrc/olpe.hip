@@ -114,11 +114,12 @@ template <int NP> struct WaveSlice {
   static constexpr int U32 = 2 * NP;                         // 8-byte multiple for NP 16/19
   static constexpr int PS = NP + 1;
   static constexpr int NSRC = NP == 16 ? 2 : 3;
-  // doubles: params[PS] | T1[3] T2[3] | C1[3] C2[3] | pending T[3] C[3] | proposal[PS]
-  static constexpr int OT1 = PS, OT2 = PS + 3, OC1 = PS + 6, OC2 = PS + 9;
-  static constexpr int OPT = PS + 12, OPC = PS + 15;
-  static constexpr int OPR = PS + 18;
-  static constexpr int F64 = 2 * PS + 18;
+  // doubles: params[PS] | T1[5] T2[5] | C1[3] C2[3] | pending T[5] C[3] | proposal[PS];
+  // a shape set's T holds cos^2, sin^2, sin 2theta and (FAST) 1/sigma_x^2, 1/sigma_y^2
+  static constexpr int OT1 = PS, OT2 = PS + 5, OC1 = PS + 10, OC2 = PS + 13;
+  static constexpr int OPT = PS + 16, OPC = PS + 21;
+  static constexpr int OPR = PS + 24;
+  static constexpr int F64 = 2 * PS + 24;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
   static constexpr int OCC = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;  // col_coef [G][3]
   static constexpr int OPE = (OCC + 2 * NSRC * 3 * 8 + 15) & ~15;
@@ -146,6 +147,11 @@ __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1
 __device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }
 __device__ __forceinline__ void st_trig(double *s, const Trig &t) {
   s[0] = t.cost2; s[1] = t.sint2; s[2] = t.sin2t;
+}
+// a shape set's cached terms: trig + the reciprocal variances (FAST coefficients)
+__device__ __forceinline__ void st_shape(double *s, const Trig &t, double ix, double iy) {
+  st_trig(s, t);
+  s[3] = ix; s[4] = iy;
 }
 __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
   s[0] = k.a; s[1] = k.b; s[2] = k.c;
@@ -334,8 +340,8 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     wave_sync();
     if (lane == 0) {
       const Trig t1 = make_trig<FAST>(st[L::T1]), t2 = make_trig<FAST>(st[L::T2]);
-      st_trig(st + WS::OT1, t1);
-      st_trig(st + WS::OT2, t2);
+      st_shape(st + WS::OT1, t1, inv_var(st[L::S1X]), inv_var(st[L::S1Y]));
+      st_shape(st + WS::OT2, t2, inv_var(st[L::S2X]), inv_var(st[L::S2Y]));
       st_coef(st + WS::OC1, make_coef<FAST>(st[L::S1X], st[L::S1Y], t1));
       st_coef(st + WS::OC2, make_coef<FAST>(st[L::S2X], st[L::S2Y], t2));
     }
@@ -408,12 +414,13 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
           const double x = (wr * g) * 2.302585092994046;
           double e;
           if (fabs(x) < 0.0625) {
-            double p = fma(x, 1.0 / 362880, 1.0 / 40320);
-            p = fma(x, p, 1.0 / 5040);
-            p = fma(x, p, 1.0 / 720);
-            p = fma(x, p, 1.0 / 120);
-            p = fma(x, p, 1.0 / 24);
-            p = fma(x, p, 1.0 / 6);
+            // (constants as SGPR addends: fma_sc, olpe_device.h)
+            double p = fma_sc(x, 1.0 / 362880, 1.0 / 40320);
+            p = fma_sc(x, p, 1.0 / 5040);
+            p = fma_sc(x, p, 1.0 / 720);
+            p = fma_sc(x, p, 1.0 / 120);
+            p = fma_sc(x, p, 1.0 / 24);
+            p = fma_sc(x, p, 1.0 / 6);
             p = fma(x, p, 0.5);
             p = fma(x, p, 1.0);
             e = fma(x, p, 1.0);
@@ -435,21 +442,32 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
       const int grp = (r == L::S1X || r == L::S1Y || r == L::T1) ? 1
                     : (r == L::S2X || r == L::S2Y || r == L::T2) ? 2 : 0;
+      // (FAST: from the set's cached reciprocal variances -- a sigma draw forms one
+      // reciprocal, a theta draw none; the same values as make_coef's)
+      auto set_coef = [&](int ot, int isx, int isy, int ith) -> Coef {
+        const Trig t = (r == ith) ? make_trig<FAST>(nv) : ld_trig(st + ot);
+        Coef C;
+        if constexpr (FAST) {
+          double ix = st[ot + 3], iy = st[ot + 4];
+          if (r == isx || r == isy) {
+            const double iv = inv_var(nv);
+            ix = r == isx ? iv : ix;
+            iy = r == isy ? iv : iy;
+          }
+          C = coef_inv(t, ix, iy);
+          if (lane == 0) st_shape(st + WS::OPT, t, ix, iy);
+        } else {
+          C = make_coef<FAST>(q(isx), q(isy), t);
+          if (lane == 0) st_trig(st + WS::OPT, t);
+        }
+        if (lane == 0) st_coef(st + WS::OPC, C);
+        return C;
+      };
       Coef C1p, C2p;
-      if (grp == 1) {
-        const Trig t = (r == L::T1) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT1);
-        C1p = make_coef<FAST>(q(L::S1X), q(L::S1Y), t);
-        if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C1p); }
-      } else {
-        C1p = ld_coef(st + WS::OC1);
-      }
-      if (grp == 2) {
-        const Trig t = (r == L::T2) ? make_trig<FAST>(nv) : ld_trig(st + WS::OT2);
-        C2p = make_coef<FAST>(q(L::S2X), q(L::S2Y), t);
-        if (lane == 0) { st_trig(st + WS::OPT, t); st_coef(st + WS::OPC, C2p); }
-      } else {
-        C2p = ld_coef(st + WS::OC2);
-      }
+      if (grp == 1) C1p = set_coef(WS::OT1, L::S1X, L::S1Y, L::T1);
+      else C1p = ld_coef(st + WS::OC1);
+      if (grp == 2) C2p = set_coef(WS::OT2, L::S2X, L::S2Y, L::T2);
+      else C2p = ld_coef(st + WS::OC2);
       // the step's model descriptor goes to LDS (the sweep loads each field where it is
       // used instead of holding 6*G doubles in registers across it), built lane-parallel:
       // lane g < G writes Gaussian g with make_model's operations, lane G the background
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
         if (grp) {
           double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
           double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
-          for (int k = 0; k < 3; ++k) dt[k] = st[WS::OPT + k];
+          for (int k = 0; k < 5; ++k) dt[k] = st[WS::OPT + k];
           for (int k = 0; k < 3; ++k) dc[k] = st[WS::OPC + k];
         }
       }

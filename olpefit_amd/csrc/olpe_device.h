@@ -435,25 +435,70 @@ struct Gauss {
   Coef k;
 };
 
+// sin and cos of |th| <= pi/4 without range reduction: Taylor polynomials in t = th^2
+// through th^17 (sin) and th^16 (cos), Horner form; the first omitted terms are below
+// 1.3e-19 / 2.8e-18 relative at pi/4, so both are within ~1 ulp of the correctly rounded
+// values (tools/check_sincos.py compares them with numpy over the range).  ~17 FP64
+// operations against ~70 VALU instructions of ocml's sincos (range reduction, selects).
+// The constants go in as SGPR operands (v_fma_f64 with an SGPR addend) instead of being
+// materialised in VGPRs for v_fmac.
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+}
+__device__ __forceinline__ void sincos_small(double th, double *s, double *c) {
+  const double t = th * th;
+  double p = fma_sc(t, 2.8114572543455207632e-15, -7.6471637318198164759e-13);  // 1/17!, -1/15!
+  p = fma_sc(t, p, 1.6059043836821614599e-10);     // 1/13!
+  p = fma_sc(t, p, -2.5052108385441718775e-8);     // -1/11!
+  p = fma_sc(t, p, 2.7557319223985890653e-6);      // 1/9!
+  p = fma_sc(t, p, -1.9841269841269841270e-4);     // -1/7!
+  p = fma_sc(t, p, 8.3333333333333333333e-3);      // 1/5!
+  p = fma_sc(t, p, -1.6666666666666666667e-1);     // -1/3!
+  *s = fma(th * t, p, th);
+  double q = fma_sc(t, 4.7794773323873852974e-14, -1.1470745597729724714e-11);  // 1/16!, -1/14!
+  q = fma_sc(t, q, 2.0876756987868098979e-9);      // 1/12!
+  q = fma_sc(t, q, -2.7557319223985890653e-7);     // -1/10!
+  q = fma_sc(t, q, 2.4801587301587301587e-5);      // 1/8!
+  q = fma_sc(t, q, -1.3888888888888888889e-3);     // -1/6!
+  q = fma_sc(t, q, 4.1666666666666666667e-2);      // 1/4!
+  q = fma(t, q, -0.5);
+  *c = fma(t, q, 1.0);
+}
+
 // EXACT keeps astropy's operations (np.sin(2*theta), six divisions); FAST kernels use
-// sin(2t) = 2 sin(t) cos(t) and two reciprocals (<= 2 ulp apart, within the fast
-// tolerances of DESIGN.md §5).
+// sin(2t) = 2 sin(t) cos(t), the polynomial sincos for |theta| <= pi/4 and two
+// reciprocals (<= 2 ulp apart, within the fast tolerances of DESIGN.md §5).
 template <bool FAST>
 __device__ __forceinline__ Trig make_trig(double th) {
   double s, c;
-  sincos(th, &s, &c);          // np.sin(theta), np.cos(theta): one range reduction
+  if (FAST && fabs(th) <= 0.78539816339744830962) {
+    sincos_small(th, &s, &c);
+  } else {
+    sincos(th, &s, &c);        // np.sin(theta), np.cos(theta): one range reduction
+  }
   return Trig{c * c, s * s, FAST ? 2.0 * (s * c) : sin(2. * th)};
 }
+
+// FAST coefficients from the shape's trig terms and the reciprocal variances
+// ix = 1/sigma_x^2, iy = 1/sigma_y^2 (the sampler keeps those per shape set, so a draw
+// of sigma_x recomputes one reciprocal and a draw of theta none)
+__device__ __forceinline__ Coef coef_inv(const Trig &t, double ix, double iy) {
+  Coef k;
+  k.a = 0.5 * (t.cost2 * ix + t.sint2 * iy);
+  k.b = 0.5 * (t.sin2t * (ix - iy));
+  k.c = 0.5 * (t.sint2 * ix + t.cost2 * iy);
+  return k;
+}
+__device__ __forceinline__ double inv_var(double s) { return 1.0 / (s * s); }
 
 template <bool FAST>
 __device__ __forceinline__ Coef make_coef(double sx, double sy, const Trig &t) {
   const double xstd2 = sx * sx, ystd2 = sy * sy;
   Coef k;
   if constexpr (FAST) {
-    const double ix = 1.0 / xstd2, iy = 1.0 / ystd2;
-    k.a = 0.5 * (t.cost2 * ix + t.sint2 * iy);
-    k.b = 0.5 * (t.sin2t * (ix - iy));
-    k.c = 0.5 * (t.sint2 * ix + t.cost2 * iy);
+    k = coef_inv(t, inv_var(sx), inv_var(sy));
   } else {
     k.a = 0.5 * ((t.cost2 / xstd2) + (t.sint2 / ystd2));
     k.b = 0.5 * ((t.sin2t / xstd2) - (t.sin2t / ystd2));
@@ -1266,6 +1311,16 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           voff = (cw.grp * n + jj) * 16;
         }
         auto img = [&](int r) -> double2 {
+#if defined(OLPE_DIAG_IMG_ROWS)
+          // diagnostic build only: every cutout read from the first OLPE_DIAG_IMG_ROWS
+          // rows (L1-resident), results meaningless -- what the L2-resident sampler loses
+          // to its cutout reads
+          r &= OLPE_DIAG_IMG_ROWS - 1;
+#endif
+#if defined(OLPE_DIAG_IMG_NONE)
+          // diagnostic build only: no cutout reads at all (per-row constants)
+          return make_double2(1e-3 * (double)r, 1.0 / 38.0);
+#endif
           if constexpr (NT > 64) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, r * rstep * 16, 0);
             double2 d;

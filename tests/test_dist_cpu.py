@@ -81,3 +81,22 @@ def test_shard_and_seed_helpers():
     assert list(s) == [2 ** 32 - 2, 2 ** 32 - 1, 0, 1]
     g = odist.HostGroup(0, 1)
     assert g.allmax(3.5) == 3.5 and g.broadcast("a") == "a"
+
+
+def test_bench_comm_watchdog_reports_and_exits():
+    """bench.py's watchdog of the end-of-run RCCL exchange: rank 0 prints its JSON line
+    with the timeout as comm_error and the process leaves with status 0 (the driver's
+    N > 1 line survives a hung collective)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import bench, threading, time\n"
+            "t = threading.Timer(0.2, bench._comm_timeout, (0, lambda: {'value': 1.0}, 0.2))\n"
+            "t.start()\n"
+            "time.sleep(30)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=repo, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["value"] == 1.0 and out["comm_error"].startswith("TimeoutError")
