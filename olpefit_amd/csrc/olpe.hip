@@ -138,8 +138,9 @@ __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsr
 // 2 x rows x 16 B, which fit in it); the 3-source 64x64 sampler keeps only the shape
 // tables (its V-table fallback runs the exact sweep instead) so that its LDS layout
 // fits 12 waves beside the cutout
-__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt) {
-  return (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
+__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, bool ring = false) {
+  return ring ? 2 * n * 16
+              : (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
 }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
@@ -233,10 +234,14 @@ template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // The global-memory (large cutout) variant runs 4-wave workgroups and waits on L2: it
 // is asked to fit 3 of them per CU (168 VGPRs, no spills; 3-source 128x128 +0.9 % over
 // 4 per CU at 128 VGPRs, +4.5 % over 2 per CU)
-__global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) void olpe_gibbs_kernel(GibbsArgs A) {
+// (the ring sampler, NT = 128 with 12 waves: one workgroup per CU, 168 VGPRs)
+__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : OLPE_GLOBAL_WAVES_PER_EU) void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
   constexpr int NP = L::NP, PS = L::PS;
+  // the 128x128 lockstep sampler: 12 waves share an LDS ring of the cutout (LdsRing,
+  // olpe_device.h); they take work units as batches of 12 and run their steps together
+  constexpr bool RING = NT == 128 && !LDS_IMG && WPB == 12 && FAST;
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = NT ? NT : A.n;
   const int npix = n * n;
@@ -249,9 +254,9 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
   unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
   double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
   constexpr int TABX = drawtab_extra(NT);
-  const int wstride = WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT);
+  const int wstride = WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT, RING);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
-                      (size_t)wave * wstride;
+                      (RING ? kRingBytes : 0) + (size_t)wave * wstride;
   uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
@@ -268,6 +273,8 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
   if (threadIdx.x == 0) s_prog[0] = 0u;
   __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
+  [[maybe_unused]] LdsRing ring;
+  if constexpr (RING) ring.prologue(smem + kSampHdr, A.DE, wave, lane);
   unsigned my_steps = 0;   // iterations this wave has started in this launch
   // start offset: the waves of a SIMD (wave, wave + 4, wave + 8) start a fraction of a
   // step apart so that their latency-bound control phases do not coincide
@@ -309,9 +316,31 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     rec_it0 = first < niter ? (int)first : -1;
     rec_row0 = (int)(k - A.row0);
   }
-  int u = A.queue ? take() : (int)blockIdx.x * WPB + wave;
-  // (host: W * units < 2^31)
-  for (; u < (int)K()->W * K()->units; u = K()->queue ? take() : INT_MAX) {
+  // ring sampler: the workgroup takes its units as batches of WPB (wave 0 draws the batch,
+  // an LDS word hands it to the others); s_prog[1] holds the batch, s_prog[2 + wave] the
+  // waves' iteration counts
+  auto take_batch = [&]() -> int {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (wave == 0 && lane == 0) {
+      const unsigned long long v = atomicAdd(K()->queue, 1ull) - K()->qbase;
+      s_prog[1] = v > 0x7fffffffull ? 0x7fffffffu : (unsigned)v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    return __builtin_amdgcn_readfirstlane((int)s_prog[1]);
+  };
+  const int total = (int)K()->W * K()->units;      // (host: W * units < 2^31)
+  int u = RING ? 0 : A.queue ? take() : (int)blockIdx.x * WPB + wave;
+  for (;;) {
+    bool active = true;
+    if constexpr (RING) {
+      const int bt = take_batch();
+      if (bt >= (total + WPB - 1) / WPB) break;    // uniform over the workgroup
+      u = bt * WPB + wave;
+      active = u < total;
+      if (!active) u = 0;       // an idle wave of the last batch: walker 0, read only
+    } else {
+      if (u >= total) break;
+    }
     // ---- the unit: chunk k of walker w, iterations [it_s, it_e) of this launch
     const int units = K()->units;
     const int Wn = (int)K()->W;
@@ -324,8 +353,19 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       it_s = q * k + (r * k) / units;
       it_e = q * (k + 1) + (r * (k + 1)) / units;
       // the walker's previous chunk ran on another wave: wait for its hand-off
-      if (k > 0)
+      if (k > 0 && active)
         unit_wait(K()->uflag + w, K()->utag + (unsigned)k, K()->uerr, K()->queue + 2, lane);
+    }
+    // ring sampler: the batch's waves run max(it_e - it_s) lockstep steps; a wave past
+    // its own iterations (or without a unit) keeps the phase barriers (idle steps)
+    int it_end = it_e;
+    if constexpr (RING) {
+      if (lane == 0) s_prog[2 + wave] = active ? (unsigned)(it_e - it_s) : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      unsigned mx = 0;
+      for (int j = 0; j < WPB; ++j) mx = max(mx, s_prog[2 + j]);
+      it_end = it_s + (int)__builtin_amdgcn_readfirstlane((int)mx);
+      if (!active) it_e = it_s;
     }
 #ifdef OLPE_DIAG_SPAN
     const unsigned long long span_t0 = __builtin_amdgcn_s_memrealtime();
@@ -382,7 +422,13 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long dt_last = __builtin_amdgcn_s_memtime();
 #endif
-    for (int it = it_s; it < it_e; ++it) {
+    for (int it = it_s; it < it_end; ++it) {
+      if constexpr (RING) {
+        if (it >= it_e) {
+          ring.idle_step();
+          continue;
+        }
+      }
       // the iteration's draws: randint(0, NP) (apf_step2.py:302), the proposal's gauss()
       // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
       int r0 = 0, dice_idx = 0;
@@ -521,7 +567,8 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
       const unsigned gmask = gauss_mask<NSRC>(r);
       gcache.same = gmask == 0 && grp == 0;
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
-                                                       &hcache, &ccache, gmask, &gcache);
+                                                       &hcache, &ccache, gmask, &gcache,
+                                                       RING ? &ring : nullptr);
       __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
       DT_MARK(3);
       const double chi = wave_sum(part);
@@ -606,6 +653,7 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     // ---- write back (the walker index laundered: its per-lane addresses are
     // recomputed here, not kept live across the sampler loop from the loads above)
     wave_sync();
+    if (RING && !active) continue;     // (no walker of its own in this batch)
     // (k and w recomputed from u: one SGPR live across the loop instead of three)
     asm volatile("" : "+s"(u));
     k = K()->units > 1 ? u / (int)K()->W : 0;
@@ -624,7 +672,11 @@ __global__ __launch_bounds__(WPB * 64, LDS_IMG ? 1 : OLPE_GLOBAL_WAVES_PER_EU) v
     // hand the walker to the wave that takes its next chunk
     if (k < K()->units - 1) unit_publish(K()->uflag + w, K()->utag + (unsigned)(k + 1), lane);
     wave_sync();      // the slice is reused by the wave's next walker
+    if constexpr (!RING) u = K()->queue ? take() : INT_MAX;
   }
+  // ring sampler: the DMAs of the phases after the last one land before the workgroup's
+  // LDS is released
+  if constexpr (RING) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------------
@@ -766,10 +818,10 @@ template <class T> int dev_alloc(T **p, size_t count) {
 
 // per-wave LDS of the kernel launch_gibbs_m picks: NT = n for LDS images of 32 and 64
 // pixels, otherwise NT = 0 / 128 (no extra draw-table bytes)
-size_t wave_lds(int n, int np, bool lds_img) {
+size_t wave_lds(int n, int np, bool lds_img, bool ring = false) {
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
   return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
-         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt);
+         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, ring);
 }
 
 // Chunks per walker of one launch.  A launch runs W walker chains of n_iters
@@ -811,15 +863,17 @@ int choose_units(long long W, long long slots, long long n_iters, int override_p
   return tb < 0.97 * T(1) ? best : 1;
 }
 
-size_t lds_bytes(const olpe_ctx *c, int wpb) {
-  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img) + kSampHdr;
+size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
+  if (ring) b += kRingBytes;
   return b;
 }
 
 template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
-  const size_t shm = lds_bytes(c, WPB);
+  constexpr bool RING = NT == 128 && !LDS && WPB == 12 && FAST;    // (olpe_gibbs_kernel)
+  const size_t shm = lds_bytes(c, WPB, RING);
   auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB, FAST>;
   // the dynamic-LDS limit is a per-device function attribute: set once per device
   // (contexts on several GPUs may launch from different host threads)
@@ -847,8 +901,9 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
                         ? choose_units(a.W, (long long)resident * WPB, a.n_iters, c->units_override)
                         : 1;
   // the LDS sampler always runs persistent; the L2-resident one only when it cuts the
-  // walkers into chunks (with whole walkers the hardware's workgroup dispatch is as good)
-  if (c->queue_on && c->d_queue && (LDS || units > 1)) {
+  // walkers into chunks (with whole walkers the hardware's workgroup dispatch is as good);
+  // the ring sampler always (launch_gibbs_m picks it only with the queue on)
+  if (c->queue_on && c->d_queue && (LDS || RING || units > 1)) {
     // persistent grid: as many workgroups as fit on the device at once, the work
     // units handed out by the queue
     if (blocks > resident) blocks = resident;
@@ -862,11 +917,13 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   if (q.units > 1) c->units_used = true;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
-  // the launch takes W * units + (its waves) values off the counter: the next
-  // launch's base (advanced only once the launch is in the stream)
-  if (q.queue)
-    c->qbase += (unsigned long long)a.W * (unsigned long long)q.units +
-                (unsigned long long)blocks * WPB;
+  // the launch takes W * units + (its waves) values off the counter (the ring sampler:
+  // one per batch of WPB units + one per workgroup): the next launch's base (advanced
+  // only once the launch is in the stream)
+  if (q.queue) {
+    const unsigned long long tot = (unsigned long long)a.W * (unsigned long long)q.units;
+    c->qbase += RING ? (tot + WPB - 1) / WPB + blocks : tot + (unsigned long long)blocks * WPB;
+  }
   return OLPE_OK;
 }
 
@@ -889,7 +946,15 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
       default: return launch_gibbs_t<NSRC, 0, true, 16, FAST>(c, a);
     }
   }
-  if (c->n == 128) return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
+  if (c->n == 128) {
+    // FAST: the lockstep ring sampler (the cutout streamed through LDS, one 12-wave
+    // workgroup per CU); OLPE_RING=0 or no walker queue: the L2-resident one
+    if constexpr (FAST) {
+      if (c->ring_on && c->queue_on && c->d_queue && c->d_uflag)
+        return launch_gibbs_t<NSRC, 128, false, 12, FAST>(c, a);
+    }
+    return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
+  }
   return launch_gibbs_t<NSRC, 0, false, 4, FAST>(c, a);
 }
 
@@ -1056,6 +1121,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     c->units_override = p;
   }
   if (const char *e = getenv("OLPE_BALANCE")) c->balance = atoi(e) != 0;   // A/B
+  if (const char *e = getenv("OLPE_RING")) c->ring_on = atoi(e) != 0;      // A/B, tests
   if (const char *e = getenv("OLPE_STAGGER")) c->stagger = std::max(0, std::min(1000, atoi(e)));
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 == hipSuccess)

@@ -1369,6 +1369,187 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
   return acc;
 }
 
+// ---------------------------------------------------------------------------------
+// Shared cutout ring of the 128x128 lockstep sampler (olpe_gibbs_kernel with RING).
+// The 256 KiB {D/err, 1/err} cutout does not fit LDS, and read by every wave from L2
+// it cost the sampler ~30 % of its time (the same kernel reading only
+// L1-resident rows ran 1.41x faster).  So the 12 waves of a workgroup sweep the cutout
+// in lockstep and share one LDS ring of 16-row phases (16 rows x 64 columns x 16 B =
+// 16 KiB; pass p covers columns 64p..64p+63), filled ahead by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs):
+//   * a step's sweep is 16 phases (2 column passes x 8 phases of 16 rows); the global
+//     phase counter g advances identically in every wave, idle waves included;
+//   * phase g lives in slot g % 3; at the start of phase g (begin_phase) every wave
+//     drains its own DMAs and LDS reads (s_waitcnt vmcnt(0) lgkmcnt(0)), the workgroup
+//     barriers, and then the DMA of phase g + 2 is issued into slot (g + 2) % 3 = the
+//     slot of phase g - 1, which every wave has finished reading (its rows are in
+//     registers before the wave reaches the barrier); rows w and w + 12 of the phase
+//     are wave w's share;
+//   * so the DMA of phase g is issued at barrier g - 2 and drained before barrier
+//     g - 1: phase g is readable from barrier g - 1 to barrier g + 2 (a wave may
+//     prefetch the first rows of phase g + 1 while it computes phase g).
+// The DMA is issued from inline asm: the compiler then inserts no vmcnt(0) before the
+// issuing wave's next LDS reads (it cannot tell the ring slots apart), and its own
+// counted waits stay correct because vector memory operations retire in order.
+constexpr int kRingRows = 16;                      // rows per phase
+constexpr int kRingSlot = kRingRows * 64 * 16;     // 16 KiB
+constexpr int kRingBytes = 3 * kRingSlot;
+constexpr int kRingPhases = 16;                    // phases per 128x128 sweep
+
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+struct LdsRing {
+  const double2 *base;   // slot 0 (generic pointer into LDS, for the reads)
+  unsigned lds;          // LDS byte address of slot 0 (M0 of the DMA)
+  const double2 *DW;     // the cutout in global memory, [128][128]
+  unsigned g;            // the phase begin_phase starts next (uniform)
+  int slot;              // g % 3
+  int wave;              // this wave's index in the workgroup (uniform)
+  unsigned voff;         // lane * 16
+
+  __device__ __forceinline__ void dma_row(int ph, int sl, int rr) const {
+    // row rr of phase ph: cutout row 16 (ph % 8) + rr, columns 64 ((ph / 8) % 2) + lane
+    const int row = ((ph & 7) << 4) + rr;
+    const double2 *src = DW + row * 128 + ((ph >> 3) & 1) * 64;
+    const unsigned dst = lds + (unsigned)(sl * kRingSlot + rr * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %3\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(dst), "s"(src)
+        : "memory");
+  }
+  // this wave's share of phase ph (rows wave and wave + 12) into slot sl
+  __device__ __forceinline__ void dma_phase(int ph, int sl) const {
+    dma_row(ph, sl, wave);
+    if (wave + 12 < kRingRows) dma_row(ph, sl, wave + 12);
+  }
+  // before the first phase: phases 0 and 1 into slots 0 and 1
+  __device__ __forceinline__ void prologue(unsigned char *ring_lds, const double2 *dw, int w,
+                                           int lane) {
+    base = reinterpret_cast<const double2 *>(ring_lds);
+    lds = (unsigned)(size_t)(lds_u8 *)ring_lds;
+    DW = dw;
+    wave = w;
+    voff = (unsigned)lane * 16u;
+    g = 0;
+    slot = 0;
+    dma_phase(0, 0);
+    dma_phase(1, 1);
+  }
+  // the barrier that opens phase g; returns the LDS slot (as a pointer) of phase g
+  __device__ __forceinline__ const double2 *begin_phase() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int s2 = slot == 0 ? 2 : slot - 1;       // (g + 2) % 3
+    dma_phase((int)((g + 2) & 15), s2);
+    const double2 *p = base + slot * (kRingSlot / 16);
+    ++g;
+    slot = slot == 2 ? 0 : slot + 1;
+    return p;
+  }
+  // a step without a sweep of this wave's own (idle wave, or a fallback sweep that read
+  // the cutout from global memory): the phases' barriers and DMA shares only
+  __device__ __forceinline__ void idle_step() {
+#pragma unroll 1
+    for (int k = 0; k < kRingPhases; ++k) (void)begin_phase();
+  }
+};
+
+// FAST3 sweep of a 128x128 cutout from the ring (sweep_fast3's NT > 64 form otherwise:
+// column terms from the step's col_coef coefficients, four-row update, shape-table
+// prefetch).  Two passes x 32 four-row blocks; a phase (four blocks) opens with
+// begin_phase just before its first block is prefetched.
+template <int NSRC>
+__device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, const double *htab,
+                                                   int lane, ExpTab ex, const double *colc,
+                                                   LdsRing &ring) {
+  constexpr int G = 2 * NSRC;
+  constexpr int BLK = 4, RU = 4, NB = 128 / BLK;    // 32 blocks per pass
+  const double bg = m.bg;
+  const double2 *hr = reinterpret_cast<const double2 *>(htab);
+  double acc = 0.0;
+#pragma unroll 1
+  for (int c0 = 0; c0 < 128; c0 += 64) {
+    const double xj = (double)(c0 + lane);
+    double av[G], rho[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const ColTerm t = col_term64(m.g[g], colc + 3 * g, xj, ex);
+      av[g] = m.g[g].amp * t.E;
+      rho[g] = t.R;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^4
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      rp[1][g] = rho[g];
+      rp[2][g] = rho[g] * rho[g];
+      rp[3][g] = rp[2][g] * rho[g];
+      rp[0][g] = rp[2][g] * rp[2][g];
+    }
+    auto row4 = [&](const double2 *h, const double2 *dw) {
+      double sw[RU], sn[RU];
+      sw[0] = av[0];
+      sn[0] = av[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) {
+        sw[0] = sw[0] + av[2 * s];
+        sn[0] = sn[0] + av[2 * s + 1];
+      }
+#pragma unroll
+      for (int r = 1; r < RU; ++r) {
+        sw[r] = av[2 * NSRC - 2] * rp[r][2 * NSRC - 2];
+        sn[r] = av[2 * NSRC - 1] * rp[r][2 * NSRC - 1];
+#pragma unroll
+        for (int s = NSRC - 2; s >= 0; --s) {
+          sw[r] = fma(av[2 * s], rp[r][2 * s], sw[r]);
+          sn[r] = fma(av[2 * s + 1], rp[r][2 * s + 1], sn[r]);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) av[g] = av[g] * rp[0][g];
+#pragma unroll
+      for (int r = 0; r < RU; ++r) {
+        const double mod = fma(sn[r], h[r].y, fma(sw[r], h[r].x, bg));
+        const double t = fma(-mod, dw[r].y, dw[r].x);
+        acc = fma(t, t, acc);
+      }
+    };
+    // rows of block b (0..31) of this pass: slot row (4b) % 16 of the phase's slot
+    const double2 *sp = ring.begin_phase();
+    double2 cur[BLK], nxt[BLK], hc[BLK];
+#pragma unroll
+    for (int k = 0; k < BLK; ++k) cur[k] = sp[k * 64 + lane];
+#pragma unroll 4
+    for (int b = 0; b < NB; ++b) {
+      // one block ahead only: without the fences the compiler gathers a whole phase's
+      // ring reads (64 VGPRs) ahead of its arithmetic and spills
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // the shape-table rows (wave-uniform broadcasts) are read with their block
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) hc[k] = hr[b * BLK + k];
+      if (b + 1 < NB) {
+        const int nb = b + 1;
+        if ((nb & 3) == 0) sp = ring.begin_phase();   // the next phase opens
+        const int r0 = (nb & 3) * BLK;
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) nxt[k] = sp[(r0 + k) * 64 + lane];
+      }
+      row4(hc, cur);
+      // the block's arithmetic completes here (machine sinking would otherwise gather
+      // a phase's four blocks behind its loads)
+      asm volatile("" : "+v"(acc));
+#pragma unroll
+      for (int k = 0; k < BLK; ++k) cur[k] = nxt[k];
+    }
+  }
+  return acc;
+}
+
 // FAST kernels keep the exact sweep only as the (rare) fallback, unrolled once so
 // that it does not set the kernel's register budget.
 // After an accepted step: refresh the cached column terms of the Gaussians the step
@@ -1410,7 +1591,7 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
                                         double *vtab, double *out, int n, int lane,
                                         const double *etab, HCache *hc = nullptr,
                                         ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0,
-                                        GuardCache *gc = nullptr) {
+                                        GuardCache *gc = nullptr, LdsRing *ring = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
@@ -1478,6 +1659,9 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
           return sweep_fast3<NSRC, NT, WRITE, true, WIDE>(m, img, h, out, n, lane, rows, kc,
                                                           ExpTab{etab}, cc, gmask, &pre);
       }
+      if constexpr (NT == 128 && !WRITE) {
+        if (ring) return sweep_fast3_ring<NSRC>(m, h, lane, ExpTab{etab}, cc->colc, *ring);
+      }
       return sweep_fast3<NSRC, NT, WRITE, false, WIDE>(m, img, h, out, n, lane, rows, kc,
                                                        ExpTab{etab}, cc);
     }
@@ -1485,13 +1669,21 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     // the descriptor lives in LDS: make the sweeps reload the fields they use instead
     // of keeping the guard's loads live (and spilled) across the row loop
     asm volatile("" ::: "memory");
-    if (lvl == 2) return sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
-    // (the 3-source 64x64 sampler has no room for the V table: sampler_vtab_bytes)
-    if (lvl == 1 && !(NSRC == 3 && NT == 64)) {
+    double part;
+    if (lvl == 2) {
+      part = sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
+    } else if (lvl == 1 && !(NSRC == 3 && NT == 64) && !ring) {
+      // (the 3-source 64x64 sampler and the ring sampler have no room for the V table:
+      // sampler_vtab_bytes)
       if (hc) hc->valid = false;                           // the V table overwrites vtab
-      return sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+      part = sweep_fast<NSRC, NT, WRITE>(m, img, vtab, out, n, lane);
+    } else {
+      part = sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
     }
-    return sweep_exact_dw<NSRC, NT, WRITE>(m, img, out, n, lane);
+    // the ring sampler's fallbacks read the cutout from global memory; the step still
+    // keeps the workgroup's phase barriers and this wave's DMA shares
+    if (ring) ring->idle_step();
+    return part;
   } else {
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
   }

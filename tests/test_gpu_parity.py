@@ -522,6 +522,43 @@ def test_work_units_l2_sampler(lib_loaded, monkeypatch):
             np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("units", [0, 1, 2, 7])
+def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, units):
+    """The 128x128 lockstep sampler (12 waves per workgroup sharing an LDS ring of the
+    cutout filled by LDS-DMA, olpe_device.h LdsRing) against the L2-resident sampler's
+    static mapping: 1,001 walkers (a last batch with 5 idle waves) over three launches
+    whose chunk bounds, record rows and burn-in fall at odd places, with an accept_min
+    stop -- chains, traces, final states, counters, RNG and done_at bit for bit equal."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    n, nsrc, W = 128, 3, 1001
+    img, _ = synth.make_image(n, nsrc, 0)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    out = []
+    for ring, no_queue, u in (("0", "1", 0), ("1", "0", units)):
+        monkeypatch.setenv("OLPE_RING", ring)
+        monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
+        monkeypatch.setenv("OLPE_UNITS", str(u))
+        s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+        p0[-1] = s.chi_squared(p0)
+        s.seed(3000 + np.arange(W))
+        s.set_state(np.tile(p0, (W, 1)))
+        s.enable_trace(True)
+        chains, traces = [], []
+        for it, burn, stride in ((31, 7, 5), (45, 0, 4), (17, 60, 3)):
+            chains.append(s.run(it, burn_in=burn, record_stride=stride, accept_min=4))
+            traces.append(s.trace(it))
+        out.append((chains, traces, s.get_state(), s.rng_state(), s.done_at()))
+        s.close()
+    (ca, ta, sa, ra, da), (cb, tb, sb, rb, db) = out
+    for x, y in zip(ca + ta, cb + tb):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(sa + ra, sb + rb):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(da, db)
+
+
 def test_work_units_automatic_choice(lib_loaded, monkeypatch):
     """configs[1]'s shape (4,096 walkers, 64x64, 100 iterations) is cut into 3 chunks
     per walker (4 full rounds of the 3,072 resident waves instead of 1 1/3); configs[2]
