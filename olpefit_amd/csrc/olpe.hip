@@ -138,10 +138,16 @@ __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsr
 // 2 x rows x 16 B, which fit in it); the 3-source 64x64 sampler keeps only the shape
 // tables (its V-table fallback runs the exact sweep instead) so that its LDS layout
 // fits 12 waves beside the cutout
-__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, bool ring = false) {
-  return ring ? 2 * n * 16
-              : (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
+__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt) {
+  return (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
 }
+// the ring sampler's per-wave slice: the WaveSlice fields up to the parking area, the
+// draw tables there (its sweeps park nothing) and the two FAST3 shape-table slots (no
+// V-table fallback)
+template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
+  return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
+}
+__host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
@@ -234,14 +240,17 @@ template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // The global-memory (large cutout) variant runs 4-wave workgroups and waits on L2: it
 // is asked to fit 3 of them per CU (168 VGPRs, no spills; 3-source 128x128 +0.9 % over
 // 4 per CU at 128 VGPRs, +4.5 % over 2 per CU)
-// (the ring sampler, NT = 128 with 12 waves: one workgroup per CU, 168 VGPRs)
-__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : OLPE_GLOBAL_WAVES_PER_EU) void olpe_gibbs_kernel(GibbsArgs A) {
+// (hipcc passes the second bound on as the minimum waves per SIMD; the ring sampler,
+// NT = 128 with one 12-wave workgroup per CU, keeps 3 per SIMD with 168 VGPRs)
+__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : OLPE_GLOBAL_WAVES_PER_EU)
+void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
   constexpr int NP = L::NP, PS = L::PS;
   // the 128x128 lockstep sampler: 12 waves share an LDS ring of the cutout (LdsRing,
   // olpe_device.h); they take work units as batches of 12 and run their steps together
-  constexpr bool RING = NT == 128 && !LDS_IMG && WPB == 12 && FAST;
+  constexpr bool RING = !LDS_IMG && FAST && ring_wpb(NT, WPB);
+  using Ring = LdsRing<WPB>;
   extern __shared__ __align__(16) unsigned char smem[];
   const int n = NT ? NT : A.n;
   const int npix = n * n;
@@ -254,13 +263,13 @@ __global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1
   unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
   double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
   constexpr int TABX = drawtab_extra(NT);
-  const int wstride = WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT, RING);
+  const int wstride = RING ? ring_wave_bytes<NP>(n) : WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
-                      (RING ? kRingBytes : 0) + (size_t)wave * wstride;
+                      (RING ? Ring::BYTES : 0) + (size_t)wave * wstride;
   uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
   uint32_t *s_acc = s_tries + NP;
   double *st = reinterpret_cast<double *>(wb + WS::U32 * 4);
-  double *vtab = reinterpret_cast<double *>(wb + WS::BYTES + TABX);
+  double *vtab = reinterpret_cast<double *>(wb + (RING ? WS::OPE + kDrawTabBytes : WS::BYTES + TABX));
   double *drawtab = reinterpret_cast<double *>(wb + (TABX ? WS::BYTES : WS::OPE));
   ModelDesc<NSRC> *mdl = reinterpret_cast<ModelDesc<NSRC> *>(wb + WS::OMD);
   double *colc = reinterpret_cast<double *>(wb + WS::OCC);
@@ -273,7 +282,7 @@ __global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1
   if (threadIdx.x == 0) s_prog[0] = 0u;
   __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
-  [[maybe_unused]] LdsRing ring;
+  [[maybe_unused]] Ring ring;
   if constexpr (RING) ring.prologue(smem + kSampHdr, A.DE, wave, lane);
   unsigned my_steps = 0;   // iterations this wave has started in this launch
   // start offset: the waves of a SIMD (wave, wave + 4, wave + 8) start a fraction of a
@@ -566,7 +575,7 @@ __global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1
       hcache.grp = grp;
       const unsigned gmask = gauss_mask<NSRC>(r);
       gcache.same = gmask == 0 && grp == 0;
-      const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12)>(*mdl, DE, vtab, nullptr, n, lane, etab,
+      const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask, &gcache,
                                                        RING ? &ring : nullptr);
       __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
@@ -819,9 +828,10 @@ template <class T> int dev_alloc(T **p, size_t count) {
 // per-wave LDS of the kernel launch_gibbs_m picks: NT = n for LDS images of 32 and 64
 // pixels, otherwise NT = 0 / 128 (no extra draw-table bytes)
 size_t wave_lds(int n, int np, bool lds_img, bool ring = false) {
+  if (ring) return (size_t)(np == 16 ? ring_wave_bytes<16>(n) : ring_wave_bytes<19>(n));
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
   return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
-         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, ring);
+         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt);
 }
 
 // Chunks per walker of one launch.  A launch runs W walker chains of n_iters
@@ -866,13 +876,13 @@ int choose_units(long long W, long long slots, long long n_iters, int override_p
 size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
   size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
-  if (ring) b += kRingBytes;
+  if (ring) b += wpb >= 12 ? LdsRing<12>::BYTES : LdsRing<6>::BYTES;
   return b;
 }
 
 template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
-  constexpr bool RING = NT == 128 && !LDS && WPB == 12 && FAST;    // (olpe_gibbs_kernel)
+  constexpr bool RING = !LDS && FAST && ring_wpb(NT, WPB);    // (olpe_gibbs_kernel)
   const size_t shm = lds_bytes(c, WPB, RING);
   auto k = olpe_gibbs_kernel<NSRC, NT, LDS, WPB, FAST>;
   // the dynamic-LDS limit is a per-device function attribute: set once per device
@@ -950,7 +960,9 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
     // FAST: the lockstep ring sampler (the cutout streamed through LDS, one 12-wave
     // workgroup per CU); OLPE_RING=0 or no walker queue: the L2-resident one
     if constexpr (FAST) {
-      if (c->ring_on && c->queue_on && c->d_queue && c->d_uflag)
+      // (two 6-wave workgroups per CU with rings of their own -- their control phases
+      // apart -- ran at 0.65x: the dispatcher does not pack two of them on a CU)
+      if (c->ring_wpb && c->queue_on && c->d_queue && c->d_uflag)
         return launch_gibbs_t<NSRC, 128, false, 12, FAST>(c, a);
     }
     return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
@@ -1121,7 +1133,14 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     c->units_override = p;
   }
   if (const char *e = getenv("OLPE_BALANCE")) c->balance = atoi(e) != 0;   // A/B
-  if (const char *e = getenv("OLPE_RING")) c->ring_on = atoi(e) != 0;      // A/B, tests
+  if (const char *e = getenv("OLPE_RING")) {                                // A/B, tests
+    const int v = atoi(e);
+    if (v != 0 && v != 12) {
+      olpe_destroy(c);
+      return set_err(OLPE_EINVAL, "OLPE_RING=%s: must be 0 (off) or 12 (waves per workgroup)", e);
+    }
+    c->ring_wpb = v;
+  }
   if (const char *e = getenv("OLPE_STAGGER")) c->stagger = std::max(0, std::min(1000, atoi(e)));
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 == hipSuccess)

@@ -1372,45 +1372,42 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // ---------------------------------------------------------------------------------
 // Shared cutout ring of the 128x128 lockstep sampler (olpe_gibbs_kernel with RING).
 // The 256 KiB {D/err, 1/err} cutout does not fit LDS, and read by every wave from L2
-// it cost the sampler ~30 % of its time (the same kernel reading only
-// L1-resident rows ran 1.41x faster).  So the 12 waves of a workgroup sweep the cutout
-// in lockstep and share one LDS ring of 16-row phases (16 rows x 64 columns x 16 B =
-// 16 KiB; pass p covers columns 64p..64p+63), filled ahead by LDS-DMA
-// (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs):
-//   * a step's sweep is 16 phases (2 column passes x 8 phases of 16 rows); the global
-//     phase counter g advances identically in every wave, idle waves included;
-//   * phase g lives in slot g % 3; at the start of phase g (begin_phase) every wave
+// it cost the sampler its latency.  So the WAVES waves of a workgroup
+// sweep the cutout in lockstep and share one LDS ring of two phase slots (a phase is
+// ROWS rows x 64 columns x 16 B; pass p covers columns 64p..64p+63), filled ahead by
+// LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs):
+//   * a step's sweep is PHASES phases (2 column passes x 128/ROWS); the global phase
+//     counter g advances identically in every wave, idle waves included;
+//   * phase g lives in slot g % 2; at the start of phase g (begin_phase) every wave
 //     drains its own DMAs and LDS reads (s_waitcnt vmcnt(0) lgkmcnt(0)), the workgroup
-//     barriers, and then the DMA of phase g + 2 is issued into slot (g + 2) % 3 = the
-//     slot of phase g - 1, which every wave has finished reading (its rows are in
-//     registers before the wave reaches the barrier); rows w and w + 12 of the phase
-//     are wave w's share;
-//   * so the DMA of phase g is issued at barrier g - 2 and drained before barrier
-//     g - 1: phase g is readable from barrier g - 1 to barrier g + 2 (a wave may
-//     prefetch the first rows of phase g + 1 while it computes phase g).
+//     barriers, and then the DMA of phase g + 1 is issued into slot (g + 1) % 2 = the
+//     slot of phase g - 1, whose rows every wave has in registers by then (a wave
+//     reaches the barrier as it prefetches the first rows of phase g, while it computes
+//     the last block of phase g - 1); rows r = wave (mod WAVES) are wave's share;
+//   * so the DMA of phase g is issued at barrier g - 1 and drained before barrier g.
 // The DMA is issued from inline asm: the compiler then inserts no vmcnt(0) before the
 // issuing wave's next LDS reads (it cannot tell the ring slots apart), and its own
 // counted waits stay correct because vector memory operations retire in order.
-constexpr int kRingRows = 16;                      // rows per phase
-constexpr int kRingSlot = kRingRows * 64 * 16;     // 16 KiB
-constexpr int kRingBytes = 3 * kRingSlot;
-constexpr int kRingPhases = 16;                    // phases per 128x128 sweep
+template <int WAVES> struct LdsRing {
+  static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
+  static constexpr int SLOT = ROWS * 64 * 16;
+  static constexpr int BYTES = 2 * SLOT;
+  static constexpr int PPP = 128 / ROWS;                  // phases per column pass
+  static constexpr int PHASES = 2 * PPP;                  // phases per 128x128 sweep
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
 
-typedef __attribute__((address_space(3))) unsigned char lds_u8;
-struct LdsRing {
   const double2 *base;   // slot 0 (generic pointer into LDS, for the reads)
   unsigned lds;          // LDS byte address of slot 0 (M0 of the DMA)
   const double2 *DW;     // the cutout in global memory, [128][128]
-  unsigned g;            // the phase begin_phase starts next (uniform)
-  int slot;              // g % 3
+  unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
 
   __device__ __forceinline__ void dma_row(int ph, int sl, int rr) const {
-    // row rr of phase ph: cutout row 16 (ph % 8) + rr, columns 64 ((ph / 8) % 2) + lane
-    const int row = ((ph & 7) << 4) + rr;
-    const double2 *src = DW + row * 128 + ((ph >> 3) & 1) * 64;
-    const unsigned dst = lds + (unsigned)(sl * kRingSlot + rr * 1024);
+    // row rr of phase ph: cutout row ROWS (ph % PPP) + rr, columns 64 (ph / PPP) + lane
+    const int row = (ph % PPP) * ROWS + rr;
+    const double2 *src = DW + row * 128 + (ph / PPP) * 64;
+    const unsigned dst = lds + (unsigned)(sl * SLOT + rr * 1024);
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -1422,12 +1419,13 @@ struct LdsRing {
         : "v"(voff), "s"(dst), "s"(src)
         : "memory");
   }
-  // this wave's share of phase ph (rows wave and wave + 12) into slot sl
+  // this wave's share of phase ph into slot sl
   __device__ __forceinline__ void dma_phase(int ph, int sl) const {
-    dma_row(ph, sl, wave);
-    if (wave + 12 < kRingRows) dma_row(ph, sl, wave + 12);
+#pragma unroll
+    for (int rr = 0; rr < ROWS; rr += WAVES)
+      if (rr + wave < ROWS) dma_row(ph, sl, rr + wave);
   }
-  // before the first phase: phases 0 and 1 into slots 0 and 1
+  // before the first phase: phase 0 into slot 0
   __device__ __forceinline__ void prologue(unsigned char *ring_lds, const double2 *dw, int w,
                                            int lane) {
     base = reinterpret_cast<const double2 *>(ring_lds);
@@ -1436,25 +1434,21 @@ struct LdsRing {
     wave = w;
     voff = (unsigned)lane * 16u;
     g = 0;
-    slot = 0;
     dma_phase(0, 0);
-    dma_phase(1, 1);
   }
-  // the barrier that opens phase g; returns the LDS slot (as a pointer) of phase g
+  // the barrier that opens phase g; returns phase g's slot
   __device__ __forceinline__ const double2 *begin_phase() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int s2 = slot == 0 ? 2 : slot - 1;       // (g + 2) % 3
-    dma_phase((int)((g + 2) & 15), s2);
-    const double2 *p = base + slot * (kRingSlot / 16);
+    dma_phase((int)((g + 1) % PHASES), (int)((g + 1) & 1));
+    const double2 *p = base + (g & 1) * (SLOT / 16);
     ++g;
-    slot = slot == 2 ? 0 : slot + 1;
     return p;
   }
   // a step without a sweep of this wave's own (idle wave, or a fallback sweep that read
   // the cutout from global memory): the phases' barriers and DMA shares only
   __device__ __forceinline__ void idle_step() {
 #pragma unroll 1
-    for (int k = 0; k < kRingPhases; ++k) (void)begin_phase();
+    for (int k = 0; k < PHASES; ++k) (void)begin_phase();
   }
 };
 
@@ -1462,12 +1456,13 @@ struct LdsRing {
 // column terms from the step's col_coef coefficients, four-row update, shape-table
 // prefetch).  Two passes x 32 four-row blocks; a phase (four blocks) opens with
 // begin_phase just before its first block is prefetched.
-template <int NSRC>
+template <int NSRC, int WAVES>
 __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, const double *htab,
                                                    int lane, ExpTab ex, const double *colc,
-                                                   LdsRing &ring) {
+                                                   LdsRing<WAVES> &ring) {
   constexpr int G = 2 * NSRC;
   constexpr int BLK = 4, RU = 4, NB = 128 / BLK;    // 32 blocks per pass
+  constexpr int BPP = LdsRing<WAVES>::ROWS / BLK;   // blocks per phase
   const double bg = m.bg;
   const double2 *hr = reinterpret_cast<const double2 *>(htab);
   double acc = 0.0;
@@ -1523,7 +1518,7 @@ __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, con
     double2 cur[BLK], nxt[BLK], hc[BLK];
 #pragma unroll
     for (int k = 0; k < BLK; ++k) cur[k] = sp[k * 64 + lane];
-#pragma unroll 4
+#pragma unroll BPP
     for (int b = 0; b < NB; ++b) {
       // one block ahead only: without the fences the compiler gathers a whole phase's
       // ring reads (64 VGPRs) ahead of its arithmetic and spills
@@ -1534,8 +1529,8 @@ __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, con
       for (int k = 0; k < BLK; ++k) hc[k] = hr[b * BLK + k];
       if (b + 1 < NB) {
         const int nb = b + 1;
-        if ((nb & 3) == 0) sp = ring.begin_phase();   // the next phase opens
-        const int r0 = (nb & 3) * BLK;
+        if (nb % BPP == 0) sp = ring.begin_phase();   // the next phase opens
+        const int r0 = (nb % BPP) * BLK;
 #pragma unroll
         for (int k = 0; k < BLK; ++k) nxt[k] = sp[(r0 + k) * 64 + lane];
       }
@@ -1586,12 +1581,12 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
   cc.pend = 0;
 }
 
-template <int NSRC, int NT, bool WRITE, bool FAST, bool WIDE = false>
+template <int NSRC, int NT, bool WRITE, bool FAST, bool WIDE = false, class RingT = LdsRing<12>>
 __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 *img,
                                         double *vtab, double *out, int n, int lane,
                                         const double *etab, HCache *hc = nullptr,
                                         ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0,
-                                        GuardCache *gc = nullptr, LdsRing *ring = nullptr) {
+                                        GuardCache *gc = nullptr, RingT *ring = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
 #ifdef OLPE_DIAG_NO_SWEEP
   // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so

@@ -57,7 +57,8 @@ struct olpe_ctx {
   int last_units = 1;       // chunks per walker of the last launch (olpe_last_units)
   bool units_used = false;  // some launch handed chunks between waves (check_units)
   int balance = 0;          // progress balancing (OLPE_BALANCE)
-  bool ring_on = true;      // 128x128 FAST: the lockstep LDS-ring sampler (OLPE_RING)
+  int ring_wpb = 12;        // 128x128 FAST: the lockstep LDS-ring sampler's waves per
+                            // workgroup, 0 = the L2-resident sampler (OLPE_RING)
   int stagger = 0;          // wave start offsets (OLPE_STAGGER)
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;

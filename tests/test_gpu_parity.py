@@ -522,11 +522,11 @@ def test_work_units_l2_sampler(lib_loaded, monkeypatch):
             np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("units", [0, 1, 2, 7])
-def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, units):
+@pytest.mark.parametrize("ring,units", [("12", 0), ("12", 1), ("12", 2), ("12", 7)])
+def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, ring, units):
     """The 128x128 lockstep sampler (12 waves per workgroup sharing an LDS ring of the
-    cutout filled by LDS-DMA, olpe_device.h LdsRing) against the L2-resident sampler's
-    static mapping: 1,001 walkers (a last batch with 5 idle waves) over three launches
+    cutout filled by LDS-DMA, olpe_device.h LdsRing) against the L2-resident
+    sampler's static mapping: 1,001 walkers (a last batch with idle waves) over three launches
     whose chunk bounds, record rows and burn-in fall at odd places, with an accept_min
     stop -- chains, traces, final states, counters, RNG and done_at bit for bit equal."""
     from olpefit_amd import synth
@@ -536,8 +536,8 @@ def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, units):
     img, _ = synth.make_image(n, nsrc, 0)
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
     out = []
-    for ring, no_queue, u in (("0", "1", 0), ("1", "0", units)):
-        monkeypatch.setenv("OLPE_RING", ring)
+    for rg, no_queue, u in (("0", "1", 0), (ring, "0", units)):
+        monkeypatch.setenv("OLPE_RING", rg)
         monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
         monkeypatch.setenv("OLPE_UNITS", str(u))
         s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)

@@ -75,8 +75,8 @@ def test_bench_sampler_has_no_scratch(usage, fast):
 
 
 def test_other_bench_configs_have_no_scratch(usage):
-    # configs[4] (3-source 128x128, global-memory sampler, 3 workgroups of 4 waves)
-    # and the 3-source 64x64 LDS sampler
-    for args in [(3, 128, False, 4, True), (3, 64, True, 12, True)]:
+    # configs[4] (3-source 128x128: the lockstep LDS-ring sampler of 12 waves and the
+    # global-memory sampler, 3 workgroups of 4 waves) and the 3-source 64x64 LDS sampler
+    for args in [(3, 128, False, 12, True), (3, 128, False, 4, True), (3, 64, True, 12, True)]:
         k = _kernel(usage, *args)
         assert k["scratch_insts"] == 0 and k["VGPRs Spill"] == 0, (args, k)
