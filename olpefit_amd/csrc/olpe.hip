@@ -121,8 +121,9 @@ template <int NP> struct WaveSlice {
   static constexpr int OPR = PS + 24;
   static constexpr int F64 = 2 * PS + 24;
   static constexpr int OMD = ((U32 * 4 + F64 * 8 + 15) & ~15);             // ModelDesc
-  static constexpr int OCC = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;  // col_coef [G][3]
-  static constexpr int OPE = (OCC + 2 * NSRC * 3 * 8 + 15) & ~15;
+  // col_coef [G][3], then (128 x 128) the pass-step factors exp(-64 b) [G]
+  static constexpr int OCC = (OMD + (int)sizeof(ModelDesc<NSRC>) + 15) & ~15;
+  static constexpr int OPE = (OCC + 2 * NSRC * 4 * 8 + 15) & ~15;
   static constexpr int BYTES = OPE + NSRC * 2 * 64 * 8;
 };
 // MTWave draw tables (kDrawTab doubles per wave).  Kernels with the FAST3 column-term
@@ -546,6 +547,8 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         // FAST sweeps of n = 64 / 128: the column-term coefficients of this Gaussian
         // (col_term64, row group 0 and S = 1 in both)
         if constexpr (FAST && NT >= 64) col_coef(gq, (double)(NT / 2), colc + 3 * lane);
+        // (two column passes: rho of pass 1 = rho of pass 0 x exp(-64 b), pass_rho)
+        if constexpr (FAST && NT == 128) colc[6 * NSRC + lane] = ExpTab{etab}(-64.0 * gq.k.b);
       } else if (lane == 2 * NSRC) {
         mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
       }

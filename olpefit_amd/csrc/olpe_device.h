@@ -1030,6 +1030,16 @@ __device__ __forceinline__ ColTerm col_term64(const Gauss &q, const double *cc, 
   const double xd = xj - q.x0;
   return ColTerm{ex.raw(-fma(fma(q.k.a, xd, cc[0]), xd, cc[1])), ex.raw(-fma(q.k.b, xd, cc[2]))};
 }
+// 128 x 128 sweeps, second column pass (columns j + 64): E from its exponent, rho from
+// the first pass's (held in the four-row update's powers) times the pass step
+// exp(-64 b) the descriptor lanes prepare (colc[6 NSRC + g]): one exp per
+// column-Gaussian instead of two.  Under the guards |64 b| < 340 (the per-column rho
+// bound of both passes), so the step is finite; rho is within ~1 ulp of the direct exp.
+__device__ __forceinline__ ColTerm col_term64_pass1(const Gauss &q, const double *cc, double xj,
+                                                    double rho0, double step, ExpTab ex) {
+  const double xd = xj - q.x0;
+  return ColTerm{ex.raw(-fma(fma(q.k.a, xd, cc[0]), xd, cc[1])), rho0 * step};
+}
 
 // Gaussians whose column terms a proposal of parameter r changes (bit g): a source's
 // position moves its two Gaussians, DX/DY the wide ones, a shape set its own; the
@@ -1123,6 +1133,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
   const double yr = (double)cw.grp;
   const double bg = m.bg;
   double acc = 0.0;
+  [[maybe_unused]] double rho0[G];     // NT = 128: pass 0's rho (col_term64_pass1)
   for (int c0 = 0; c0 < n; c0 += 64) {
     const int j = c0 + cw.jl;
     const bool act = cw.lane_ok && j < n;
@@ -1178,7 +1189,12 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           cc->R[g] = t.R;
           cc->valid |= 1u << g;
         }
-      } else if constexpr (NT >= 64) {      // sampler kernels (cc carries the coefficients)
+      } else if constexpr (NT == 128) {     // sampler kernels (cc carries the coefficients)
+        t = c0 == 0 ? col_term64(m.g[g], cc->colc + 3 * g, xj, ex)
+                    : col_term64_pass1(m.g[g], cc->colc + 3 * g, xj, rho0[g],
+                                       cc->colc[3 * G + g], ex);
+        rho0[g] = t.R;
+      } else if constexpr (NT >= 64) {
         t = col_term64(m.g[g], cc->colc + 3 * g, xj, ex);
       } else {
         t = col_term(m.g[g], xj, yr, S, kcd, ex);
@@ -1438,7 +1454,13 @@ template <int WAVES> struct LdsRing {
   }
   // the barrier that opens phase g; returns phase g's slot
   __device__ __forceinline__ const double2 *begin_phase() {
+#ifdef OLPE_DIAG_NO_BARRIER
+    // diagnostic build only: no barrier (the ring races, results meaningless) -- what
+    // the lockstep costs
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     dma_phase((int)((g + 1) % PHASES), (int)((g + 1) & 1));
     const double2 *p = base + (g & 1) * (SLOT / 16);
     ++g;
@@ -1466,15 +1488,19 @@ __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, con
   const double bg = m.bg;
   const double2 *hr = reinterpret_cast<const double2 *>(htab);
   double acc = 0.0;
+  double rho0[G];                      // pass 0's rho (col_term64_pass1)
 #pragma unroll 1
   for (int c0 = 0; c0 < 128; c0 += 64) {
     const double xj = (double)(c0 + lane);
     double av[G], rho[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const ColTerm t = col_term64(m.g[g], colc + 3 * g, xj, ex);
+      const ColTerm t = c0 == 0 ? col_term64(m.g[g], colc + 3 * g, xj, ex)
+                                : col_term64_pass1(m.g[g], colc + 3 * g, xj, rho0[g],
+                                                   colc[3 * G + g], ex);
       av[g] = m.g[g].amp * t.E;
       rho[g] = t.R;
+      rho0[g] = t.R;
       __builtin_amdgcn_sched_barrier(0);
     }
     double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^4
