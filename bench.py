@@ -213,6 +213,10 @@ def main():
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0, no RCCL "
                          "all-gather (RCCL refuses two ranks on one device)")
+    ap.add_argument("--share-gpu-rccl", action="store_true",
+                    help="rehearsal of the exchange's error path: every rank on device 0 "
+                         "and the RCCL exchange attempted (RCCL refuses it; the line "
+                         "carries comm_error)")
     args = ap.parse_args()
     # configs[1]'s launch is ~0.85 ms: the chip raises its clock only under sustained
     # load (in-kernel s_memtime/s_memrealtime: ~1.9 GHz over the first ~10 ms of work,
@@ -236,7 +240,8 @@ def main():
     if args.walkers:
         wpg = args.walkers
     img, _ = synth.make_image(n, nsrc, 0)
-    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=0 if args.share_gpu else local)
+    shared = args.share_gpu or args.share_gpu_rccl
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=0 if shared else local)
     # step-1 style start (apf_step2.py:264-289) for every walker
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
