@@ -187,3 +187,43 @@ def test_cli_resume_after_interrupt(tmp_path, monkeypatch, mode):
         np.testing.assert_array_equal(np.load(cut + f"{w}_chain.npy"),
                                       np.load(ref + f"{w}_chain.npy"))
     assert not os.path.exists(cut + "step2_checkpoint.npz")
+
+
+_RSS_RUN = r"""
+import resource, sys
+sys.path.insert(0, {repo!r})
+from olpefit_amd import step2
+out = step2.main([{path!r}, "--walkers", "1024", "--seed", "5", "--iters", "{iters}",
+                  "--burn-in", "0", "--record-stride", "10", "--chunk", "500", "--no-csv",
+                  "--npy", "-q"])
+print(out)
+print(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss)
+"""
+
+
+def test_cli_host_memory_bounded_by_launch(tmp_path):
+    """Streamed output (apf_step2.py:342-365 without the O(n^2) rewrite): 1,024 walkers
+    for 1,000 and for 8,000 iterations (stride 10, launches of 500) -- the chain on disk
+    grows by 95 MB, the process's peak RSS by far less than that (one launch's rows are
+    7 MB), and every walker's .npy holds all its rows."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rss = {}
+    for iters in (1000, 8000):
+        d = tmp_path / f"r{iters}"
+        d.mkdir()
+        path = synth.write_case(str(d), 32, 2)
+        r = subprocess.run([sys.executable, "-c", _RSS_RUN.format(repo=repo, path=path,
+                                                                   iters=iters)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = r.stdout.strip().splitlines()
+        rss[iters] = int(lines[-1]) * 1024                             # ru_maxrss: KiB
+        out = lines[-2]
+        for w in (0, 1023):
+            c = np.load(out + f"{w}_chain.npy")
+            assert c.shape[1] == 17 and c.shape[0] in (iters // 10, iters // 10 + 1)
+            assert np.all(np.isfinite(c[-iters // 10:]))
+    grow = rss[8000] - rss[1000]
+    assert grow < 40e6, (rss, grow)
