@@ -407,11 +407,20 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     mt.gauss = uniform_f64(K()->gauss[w]);
     mt.tab = drawtab;
 
+    // accept_min stop (apf_step2.py:300): done_at = the first count at which every
+    // parameter has been tried accept_min times.  Touched only when ndone changes (a
+    // draw whose tries reach accept_min, once per parameter), so that the step carries
+    // no per-iteration VALU work for it and no wait on done_at's load: a per-iteration
+    // test kept done_at in VGPRs and made every iteration wait vmcnt(0) -- also on the
+    // chain-row stores of the iteration before
     int ndone = 0;
     long long done_at = K()->done_at[w];
     if (A.accept_min > 0) {
       for (int k = 0; k < NP; ++k) ndone += (s_tries[k] >= (uint32_t)A.accept_min);
       ndone = __builtin_amdgcn_readfirstlane(ndone);
+      // every parameter tried accept_min times before this unit (a launch with
+      // accept_min after one without): done at the end of the unit's first iteration
+      if (ndone == NP && done_at < 0 && it_s < it_e) done_at = A.count0 + it_s + 1;
     }
 
     int rec_it = rec_it0, rec_row = rec_row0;
@@ -455,7 +464,9 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
       wave_sync();
       if (lane == 0) s_tries[r] = tr;
-      if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) ++ndone;
+      if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) {
+        if (++ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
+      }
       DT_MARK(0);
 
       // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
@@ -620,7 +631,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         }
       }
       wave_sync();
-      if (A.accept_min > 0 && ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
       DT_MARK(5);
 
 #if !defined(OLPE_DIAG_TIMING) && !defined(OLPE_DIAG_SPAN)
