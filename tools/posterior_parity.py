@@ -2,9 +2,11 @@
 means / sigmas of the GPU chains against the NumPy reference on identical seeds).
 
     python tools/posterior_parity.py [--walkers 16] [--iters 2000] [--burn 500] [--mode fast]
+                                     [--config 2|4]
 
 Runs W walkers (seeds 1000 + w, the bench's step-1 style start) on the synthetic 64x64
-two-source cutout through libolpe, and the same walkers through the oracle
+two-source cutout (--config 4: the 128x128 three-source one, on the lockstep ring
+sampler) through libolpe, and the same walkers through the oracle
 (oracle/olpe_oracle.py, one process per walker), then prints per-parameter posterior
 mean and sigma of the pooled chains, their differences, and the truth the frame was
 rendered from.  The oracle is the checker here, never the thing measured.
@@ -23,25 +25,28 @@ sys.path.insert(0, REPO)
 
 NAMES = ["xcs", "ycs", "xcc", "ycc", "dx", "dy", "amps", "ampc", "ratio", "bkgd",
          "sx", "sy", "sx2", "sy2", "th", "th2"]
+# 3-source layout (3body/apf_step2_3body.py:266-288)
+NAMES3 = ["x1", "y1", "x2", "y2", "x3", "y3", "dx", "dy", "amp1", "amp2", "amp3", "ratio",
+          "bkgd", "sx", "sy", "sx2", "sy2", "th", "th2"]
 
 
-def _setup(n):
+def _setup(n, nsrc):
     from olpefit_amd import synth
     from olpefit_amd.pipeline import initial_parameters
     from oracle import olpe_oracle as ora
-    img, _ = synth.make_image(n, 2, 0)
+    img, _ = synth.make_image(n, nsrc, 0)
     dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
-    p0 = initial_parameters(img, synth.guess_values(n, 2), 2)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
     with np.errstate(all="ignore"):
-        p0[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p0, n), err))
+        p0[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p0, n, nsrc), err))
     return img, dm, err, p0
 
 
 def _oracle_walker(args):
-    n, seed, iters, burn = args
+    n, nsrc, seed, iters, burn = args
     from oracle import olpe_oracle as ora
-    _, dm, err, p0 = _setup(n)
-    chain, _ = ora.Walker(dm, err, p0, seed).run(iters, burn_in=burn)
+    _, dm, err, p0 = _setup(n, nsrc)
+    chain, _ = ora.Walker(dm, err, p0, seed, nsrc=nsrc).run(iters, burn_in=burn)
     return chain
 
 
@@ -51,31 +56,34 @@ def main():
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--burn", type=int, default=500)
     ap.add_argument("--mode", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4])
     args = ap.parse_args()
-    n = 64
+    n, nsrc = (64, 2) if args.config == 2 else (128, 3)
+    names = NAMES if nsrc == 2 else NAMES3
+    npar = len(names)
     from olpefit_amd import synth
     from olpefit_amd.core import Sampler
-    img, dm, err, p0 = _setup(n)
+    img, dm, err, p0 = _setup(n, nsrc)
     seeds = 1000 + np.arange(args.walkers)
-    s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
     s.set_eval_mode(args.mode)
     s.seed(seeds)
     s.set_state(np.tile(p0, (args.walkers, 1)))
     gpu = s.run(args.iters, burn_in=args.burn, record_stride=1)
     with mp.get_context("spawn").Pool(min(16, args.walkers)) as pool:
-        ref = np.stack(pool.map(_oracle_walker, [(n, int(sd), args.iters, args.burn)
+        ref = np.stack(pool.map(_oracle_walker, [(n, nsrc, int(sd), args.iters, args.burn)
                                                  for sd in seeds]))
     assert gpu.shape == ref.shape, (gpu.shape, ref.shape)
-    g = gpu.reshape(-1, gpu.shape[-1])[:, :16]
-    r = ref.reshape(-1, ref.shape[-1])[:, :16]
-    truth = synth.truth_params(n, 2)
+    g = gpu.reshape(-1, gpu.shape[-1])[:, :npar]
+    r = ref.reshape(-1, ref.shape[-1])[:, :npar]
+    truth = synth.truth_params(n, nsrc)
     print(f"{args.walkers} walkers x {args.iters} iterations (burn-in {args.burn}), "
-          f"{args.mode} evaluation, 64x64 two-source synthetic cutout; "
+          f"{args.mode} evaluation, {n}x{n} {nsrc}-source synthetic cutout; "
           f"{g.shape[0]} pooled samples")
     print(f"{'param':>6} {'truth':>12} {'mean gpu':>16} {'mean ref':>16} {'|dmean|':>9} "
           f"{'sigma gpu':>12} {'|dsigma|/sigma':>14}")
     worst = 0.0
-    for k, name in enumerate(NAMES):
+    for k, name in enumerate(names):
         mg, mr = g[:, k].mean(), r[:, k].mean()
         sg, sr = g[:, k].std(), r[:, k].std()
         ds = abs(sg - sr) / sr if sr > 0 else abs(sg - sr)
@@ -84,7 +92,7 @@ def main():
               f"{sg:12.6g} {ds:14.2e}")
     same = np.mean(np.isclose(gpu, ref, rtol=1e-8, atol=1e-9))
     print(f"max relative |dmean| {worst:.2e}; centroid |dmean| (px) "
-          f"{max(abs(g[:, k].mean() - r[:, k].mean()) for k in range(4)):.2e}; "
+          f"{max(abs(g[:, k].mean() - r[:, k].mean()) for k in range(2 * nsrc)):.2e}; "
           f"chain entries equal to rtol 1e-8: {same * 100:.4f} %")
 
 
