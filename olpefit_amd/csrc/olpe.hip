@@ -589,6 +589,9 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       hcache.grp = grp;
       const unsigned gmask = gauss_mask<NSRC>(r);
       gcache.same = gmask == 0 && grp == 0;
+      // (per-column guard cache: the Gaussians this draw moves or reshapes -- a shape
+      // set is the narrow Gaussians, odd g, or the wide ones, even g)
+      gcache.changed = gmask | (grp == 1 ? 0xAAAu : grp == 2 ? 0x555u : 0u) & ((1u << (2 * NSRC)) - 1u);
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask, &gcache,
                                                        RING ? &ring : nullptr);
@@ -920,7 +923,10 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
   const unsigned resident = (unsigned)std::max(1, per_cu) * (unsigned)c->n_cu;
-  const int units = c->queue_on && c->d_queue && c->d_uflag
+  // (ring sampler: a batch's 12 units run in lockstep, so a chunk must never wait on its
+  // predecessor inside its own batch -- the predecessor of unit u is u - W, in an earlier
+  // batch whenever W >= 12; fewer walkers run whole)
+  const int units = c->queue_on && c->d_queue && c->d_uflag && !(RING && a.W < WPB)
                         ? choose_units(a.W, (long long)resident * WPB, a.n_iters, c->units_override)
                         : 1;
   // the LDS sampler always runs persistent; the L2-resident one only when it cuts the

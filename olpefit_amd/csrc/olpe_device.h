@@ -942,6 +942,55 @@ __device__ __forceinline__ bool fast3_ok_cols(const ModelDesc<NSRC> &m, int n, i
   return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
+// The per-column test of fast3_ok_cols for each Gaussian of `which`, without its
+// amplitude bound: returns the Gaussians that pass.  Their result is a function of the
+// Gaussian's centre and shape only, so the sampler keeps it per Gaussian across steps
+// (GuardCache::colok) and retests only the Gaussians a draw moves or reshapes; the
+// amplitude bound (|A| < 1e20) is checked every step (fast3_amp_ok).
+template <int NSRC>
+__device__ __forceinline__ unsigned fast3_cols_pass(const ModelDesc<NSRC> &m, int n, int rows, int kc,
+                                                   int lane, unsigned which) {
+  const ColWalk cw(n, lane);
+  const double S = (double)cw.S;
+  const double kcd = (double)kc;
+  const double km = (double)(kc > rows - 1 - kc ? kc : rows - 1 - kc) + 1.0;
+  const double yr = (double)cw.grp;
+  unsigned passed = 0;
+#pragma unroll 1
+  for (unsigned f = which; f; f &= f - 1u) {
+    const int g = __builtin_ctz(f);
+    const Gauss &q = m.g[g];
+    const double cs = q.k.c * (S * S);
+    const double K = cs * (kcd * (kcd + 1.0));
+    const double amin = q.k.a - (q.k.b * q.k.b) / (4.0 * q.k.c);
+    const double yd = yr - q.y0;
+    int ok = (int)(cs * km * km < 600.0) & (int)(q.k.a >= 0.0) & (int)(q.k.c > 0.0) &
+             (int)isfinite(amin);
+#pragma unroll 1
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int j = c0 + cw.jl;
+      const bool act = cw.lane_ok && j < n;
+      const double xd = (double)j - q.x0;
+      const double bx = q.k.b * xd;
+      const double q0 = (q.k.a * (xd * xd) + bx * yd) + q.k.c * (yd * yd);
+      const double d0 = bx * S + (q.k.c * S) * (2.0 * yd + S);
+      const double xe = K - q0;
+      const double xr = d0 + 2.0 * cs * kcd;
+      const int okc = (int)(fabs(xr) < 170.0) & ((int)(xe > -700.0) | (int)(amin * (xd * xd) >= 100.0));
+      ok &= okc | (int)!act;
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) passed |= 1u << g;
+  }
+  return passed;
+}
+// fast3_ok_cols's amplitude bound for the Gaussians of `which` (lane-parallel)
+template <int NSRC>
+__device__ __forceinline__ bool fast3_amp_ok(const ModelDesc<NSRC> &m, int lane, unsigned which) {
+  const bool bad = lane < 2 * NSRC && ((which >> lane) & 1u) &&
+                   !(fabs(m.g[lane < 2 * NSRC ? lane : 0].amp) < 1e20);
+  return __builtin_amdgcn_ballot_w64(bad) == 0;
+}
+
 // FAST3's shape tables, tab[2k] = H_wide(k), tab[2k+1] = H_narrow(k), k lane-parallel.
 // `which` selects the sets recomputed (bit 0 wide, bit 1 narrow); the others are copied
 // from `from` (the table of the current state: a Gibbs step changes at most one set).
@@ -975,11 +1024,20 @@ struct GuardCache {
   bool same = false;    // this step's draw leaves the guard inputs unchanged
   bool valid = false;   // cur holds the current state's guard
   bool cur = false, prop = false;
+  // per-column guard (cutouts wider than 64): colok = the Gaussians known to pass
+  // fast3_cols_pass in the current state; changed = the Gaussians this step's draw
+  // moves or reshapes; colprop / coltest = the proposal's known passes / this step's
+  // tested ones
+  unsigned colok = 0, changed = 0, colprop = 0, coltest = 0;
   __device__ __forceinline__ void after(bool accepted) {
     if (same || accepted) {
       cur = prop;
       valid = true;
     }
+    // an accept makes the proposal's results current; after a reject the results of
+    // Gaussians the draw left unchanged still hold
+    colok = accepted ? colprop : (colok & ~changed) | (coltest & ~changed);
+    coltest = 0;
   }
 };
 
@@ -1646,7 +1704,20 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       ok3 = fails == 0;
       if (!ok3) {
         asm volatile("" ::: "memory");
-        ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane, fails);
+        if (gc) {
+          // per Gaussian: the column test's result for an unchanged Gaussian is reused
+          const unsigned keep = gc->colok & ~gc->changed;
+          const unsigned need = fails & ~keep;
+          const unsigned passed = need ? fast3_cols_pass<NSRC>(m, nn, rows0, kc, lane, need) : 0u;
+          gc->coltest = passed;
+          gc->colprop = keep | passed;
+          ok3 = (fails & ~(keep | passed)) == 0 && fast3_amp_ok<NSRC>(m, lane, fails);
+        } else {
+          ok3 = fast3_ok_cols<NSRC>(m, nn, rows0, kc, lane, fails);
+        }
+      } else if (gc) {
+        gc->coltest = 0;
+        gc->colprop = gc->colok & ~gc->changed;
       }
     } else {
       if (gc && gc->same && gc->valid) ok3 = gc->cur;

@@ -559,6 +559,35 @@ def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, ring, units):
     np.testing.assert_array_equal(da, db)
 
 
+def test_ring_sampler_few_walkers_forced_units(lib_loaded, monkeypatch):
+    """A lockstep batch must not hold a chunk and its predecessor (the chunk would wait
+    for a wave that waits at the batch's barrier): with fewer walkers than a batch the
+    ring sampler runs whole walkers even when chunks are forced -- 5 walkers with
+    OLPE_UNITS=3 finish (no hand-off timeout) and equal the L2 sampler's run."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    n, nsrc, W = 128, 3, 5
+    img, _ = synth.make_image(n, nsrc, 0)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    out = []
+    for rg, no_queue in (("0", "1"), ("12", "0")):
+        monkeypatch.setenv("OLPE_RING", rg)
+        monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
+        monkeypatch.setenv("OLPE_UNITS", "3")
+        s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+        p0[-1] = s.chi_squared(p0)
+        s.seed(4000 + np.arange(W))
+        s.set_state(np.tile(p0, (W, 1)))
+        c = s.run(60, burn_in=0, record_stride=3)
+        out.append((c, s.get_state(), s.rng_state(), s.last_units()))
+        s.close()
+    assert out[1][3] == 1
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for x, y in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_work_units_automatic_choice(lib_loaded, monkeypatch):
     """configs[1]'s shape (4,096 walkers, 64x64, 100 iterations) is cut into 3 chunks
     per walker (4 full rounds of the 3,072 resident waves instead of 1 1/3); configs[2]
