@@ -424,6 +424,38 @@ struct ExpTab {
   }
 };
 
+// exp(-q) of the EXACT sweeps, q = the Gaussian's quadratic form (>= 0 up to rounding,
+// or NaN, +inf).  The operations of ocml's exp, so the same bits: k = rint(-q log2 e),
+// r = -q - k ln2 in two FMAs, 1 + r p(r) with p of degree 10, then 2^k by ldexp.  What is
+// left out are ocml's range selects (two compares, three selects per call): an
+// argument beyond the underflow point (q > 745.13) gives 0 through the ldexp (k <=
+// -1075) as long as the reduction stays exact, so q > 1000 is clamped in its high word
+// (one compare, one 32-bit select; the low word keeps q within [1000, 1000.0000001]),
+// and NaN passes the compare and the reduction unchanged.  tools/micro/exp_check.hip
+// compares it with ocml's exp bit for bit.  (A q far below 0 -- a quadratic form that
+// rounding leaves negative by more than ~709 -- would give NaN where ocml gives inf;
+// both make chi^2 reject the proposal.)
+__device__ __forceinline__ double exp_neg(double q) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(q);
+  const unsigned hi = q > 1000.0 ? 0x408F4000u : (unsigned)(b >> 32);
+  q = __longlong_as_double((long long)(((unsigned long long)hi << 32) | (b & 0xffffffffull)));
+  const double k = __builtin_rint(q * -0x1.71547652b82fep+0);
+  double r = fma(k, -0x1.62e42fefa39efp-1, -q);
+  r = fma(-0x1.abc9e3b39803fp-56, k, r);
+  double p = fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
+  p = fma(r, p, 0x1.71dee623fde64p-19);
+  p = fma(r, p, 0x1.a01997c89e6b0p-16);
+  p = fma(r, p, 0x1.a01a014761f6ep-13);
+  p = fma(r, p, 0x1.6c16c1852b7b0p-10);
+  p = fma(r, p, 0x1.1111111122322p-7);
+  p = fma(r, p, 0x1.55555555502a1p-5);
+  p = fma(r, p, 0x1.5555555555511p-3);
+  p = fma(r, p, 0x1.000000000000bp-1);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  return ldexp(p, (int)k);
+}
+
 struct Trig {
   double cost2, sint2, sin2t;
 };
@@ -585,7 +617,7 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
       for (int g = 0; g < G; ++g) {
         const double yd = yi - m.g[g].y0;
         const double qq = (t1[g] + t2[g] * yd) + m.g[g].k.c * (yd * yd);
-        v[g] = m.g[g].amp * exp(-qq);
+        v[g] = m.g[g].amp * exp_neg(qq);
       }
       double mod = v[0] + v[1];
 #pragma unroll
@@ -627,7 +659,7 @@ __device__ __forceinline__ double sweep_exact_dw(const ModelDesc<NSRC> &m, const
         const double yd = yi - m.g[g].y0;
         const double qq = (m.g[g].k.a * (xd * xd) + (m.g[g].k.b * xd) * yd) +
                           m.g[g].k.c * (yd * yd);
-        v[g] = m.g[g].amp * exp(-qq);
+        v[g] = m.g[g].amp * exp_neg(qq);
       }
       double mod = v[0] + v[1];
 #pragma unroll
