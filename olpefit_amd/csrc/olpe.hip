@@ -658,6 +658,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
 #ifdef OLPE_DIAG_TIMING
     if (A.trace && lane < 9) {
       unsigned long long v = lane == 7 ? ccache.n_setup : lane == 8 ? ccache.n_refresh : 0;
+      if constexpr (RING) v = lane == 7 ? ring.wait_first : lane == 8 ? ring.wait_rest : v;
       for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
       A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
     }

@@ -1508,6 +1508,11 @@ template <int WAVES> struct LdsRing {
   unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
+#ifdef OLPE_DIAG_TIMING
+  // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
+  // phase of a step (behind the workgroup's slowest control section) and at the others
+  unsigned long long wait_first = 0, wait_rest = 0;
+#endif
 
   __device__ __forceinline__ void dma_row(int ph, int sl, int rr) const {
     // row rr of phase ph: cutout row ROWS (ph % PPP) + rr, columns 64 (ph / PPP) + lane
@@ -1549,7 +1554,15 @@ template <int WAVES> struct LdsRing {
     // the lockstep costs
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #else
+#ifdef OLPE_DIAG_TIMING
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifdef OLPE_DIAG_TIMING
+    const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t0;
+    if (g % PHASES == 0) wait_first += dtw;
+    else wait_rest += dtw;
+#endif
 #endif
     dma_phase((int)((g + 1) % PHASES), (int)((g + 1) & 1));
     const double2 *p = base + (g & 1) * (SLOT / 16);
