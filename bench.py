@@ -58,14 +58,18 @@ CONFIG_NAMES = {
 }
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
 HBM_PEAK = 8.0e12                 # MI355X HBM3E spec (MI355X_MICROARCH.md)
-EXP_OPS = 19                      # FP64 VALU ops of one ocml exp(f64), ISA count
+# one exp of the EXACT sweep (olpe::exp_neg, ocml's sequence without its range selects):
+EXP_OPS = 16                      # FP64 VALU instructions, ISA count (mul, rint, 2 + 11 fma,
+                                  # ldexp): SURVEY.md 8(d)'s E
+EXP_LANE_OPS = 14                 # of them in the SQ FP64 classes (FMA/MUL/ADD; rint and
+                                  # ldexp are not): the operation count stays a lower bound
 EXP_TAB_OPS = 12                  # FP64 VALU ops of olpe::exp_tab (FAST3 setup)
 
 
 def work_per_step(n: int, nsrc: int, mode: str) -> float:
     """FP64 VALU lane-ops of one walker-step's model + chi^2 evaluation.
 
-    exact: per pixel-Gaussian 7 ops + one exp (E = 19), per pixel G-1 combines +
+    exact: per pixel-Gaussian 7 ops + one exp (14 counted ops), per pixel G-1 combines +
            background + 3 residual ops, per column-Gaussian 4 hoisted ops.
     fast:  the FAST3 sweep every guarded step of this workload takes: per pixel, with
            the four-row update, 2 sets x (5m-1)/4 (m = nsrc Gaussians per set; G
@@ -77,7 +81,7 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
            rebuilt for one set (one exp + 3 ops per row) on the 6 draws that change one."""
     g = 2 * nsrc
     if mode == "exact":
-        return n * n * (g * (7 + EXP_OPS) + g + 3) + 4 * n * g
+        return n * n * (g * (7 + EXP_LANE_OPS) + g + 3) + 4 * n * g
     np_ = 16 if nsrc == 2 else 19
     changed = (12 * 2 if nsrc == 2 else (6 * 2 + 2 * 3 + 6 * 3)) / np_
     if n > 64:                       # two column passes: no column-term cache
@@ -335,7 +339,7 @@ def main():
                 "per walker-step, FMA counted once) x HIP-event rate / 78.6e12/2; "
                 "valu_issue_frac = all VALU instructions x 64 / the same peak; model_chi2_frac = "
                 "the model + chi^2 operations alone (DESIGN.md §4); equivalent_exp_form_rate = "
-                "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 19) at this rate, in T "
+                "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 16) at this rate, in T "
                 "lane-ops/s: FAST does far fewer operations, so it is no utilisation figure; "
                 "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
                 "(profiles/pmc_traffic.json); the north star's >= 40 % HBM-read roofline does "
