@@ -150,6 +150,10 @@ template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
 }
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
+// the 2-source 64x64 EXACT sampler's row tables (sweep_exact_rows): [64][4] doubles in
+// the parking area and in the V-table area
+static_assert(WaveSlice<16>::BYTES - WaveSlice<16>::OPE >= 64 * 4 * 8 &&
+              sampler_vtab_bytes(64, 2, 64) >= 64 * 4 * 8, "sweep_exact_rows tables");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
 __device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }

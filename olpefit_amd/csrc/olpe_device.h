@@ -635,6 +635,61 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
   return acc;
 }
 
+// sweep_exact of the 64x64 EXACT sampler with the row terms from LDS: dy = i - y0 and
+// c*(dy*dy) depend on the row and the Gaussian only, so the wave forms them once per
+// step, lane = row (3 operations per Gaussian for all 64 rows), into ytab / qtab
+// ([64][G] each, LDS the EXACT sampler leaves unused), and each row reads them as
+// wave-uniform broadcasts: 3 operations per pixel and Gaussian for the quadratic form
+// instead of 6, the same operations on the same values, so the same bits.
+template <int NSRC>
+__device__ __forceinline__ double sweep_exact_rows(const ModelDesc<NSRC> &m, const double2 *DE,
+                                                   int lane, double *ytab, double *qtab) {
+  constexpr int G = 2 * NSRC;
+  {
+    const double yi = (double)lane;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double yd = yi - m.g[g].y0;
+      ytab[lane * G + g] = yd;
+      qtab[lane * G + g] = m.g[g].k.c * (yd * yd);
+    }
+  }
+  wave_sync();
+  const double xj = (double)lane;
+  double t1[G], t2[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const double xd = xj - m.g[g].x0;
+    t1[g] = m.g[g].k.a * (xd * xd);
+    t2[g] = m.g[g].k.b * xd;
+  }
+  // the tables' LDS addresses in VGPRs, so that each row's reads are a VGPR base plus
+  // immediate offsets (from SGPR bases the compiler copies every address to a VGPR)
+  typedef __attribute__((address_space(3))) const double lds_f64;
+  lds_f64 *yl = (lds_f64 *)ytab;
+  lds_f64 *ql = (lds_f64 *)qtab;
+  asm volatile("" : "+v"(yl), "+v"(ql));
+  double acc = 0.0;
+#pragma unroll 2
+  for (int i = 0; i < 64; ++i) {
+    double v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double qq = (t1[g] + t2[g] * yl[i * G + g]) + ql[i * G + g];
+      v[g] = m.g[g].amp * exp_neg(qq);
+    }
+    double mod = v[0] + v[1];
+#pragma unroll
+    for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
+    mod = mod + m.bg;
+    const double2 de = DE[i * 64 + lane];
+    const double t = (de.x - mod) * de.y;
+    acc = fma(t, t, acc);
+  }
+  wave_sync();   // the tables are rewritten by the next step
+  return acc;
+}
+
 // Exact per-pixel model with the fast kernels' {D/err, 1/err} image: the fallback of
 // FAST kernels for steps that fail both fast guards (residual in the fma form).
 template <int NSRC, int NT, bool WRITE>
@@ -1822,6 +1877,11 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     if (ring) ring->idle_step();
     return part;
   } else {
+    // (the 2-source 64x64 sampler: row tables in its column-term parking area and V
+    // table, both unused in EXACT -- 2 KiB each)
+    if constexpr (NT == 64 && NSRC == 2 && !WRITE) {
+      if (cc) return sweep_exact_rows<NSRC>(m, img, lane, cc->pbuf, vtab);
+    }
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
   }
 }

@@ -671,6 +671,31 @@ def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core):
         assert np.array_equal(tr[w, :, 5] > 0.5, np.array([t[4] for t in rtr], bool))
 
 
+@pytest.mark.parametrize("n,nsrc", [(64, 2), (64, 3), (32, 2), (128, 3)])
+def test_exact_sampler_chi2_bitwise_equals_eval(lib_loaded, n, nsrc):
+    """The EXACT sampler's sweeps (the 64x64 2-source one with its LDS row tables,
+    sweep_exact_rows; the others sweep_exact) perform the operations of the EXACT eval
+    kernel (olpe_chi2_batch) on the same values: every recorded chain row's chi^2 equals
+    olpe_chi2_batch of that row's parameters bit for bit."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    W, n_it = 96, 60
+    img, _ = synth.make_image(n, nsrc, 0)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode("exact")
+    p0[-1] = s.chi_squared(p0)
+    s.seed(7000 + np.arange(W))
+    s.set_state(np.tile(p0, (W, 1)))
+    chain = s.run(n_it, burn_in=0, record_stride=3)
+    rows = chain.reshape(-1, s.ps)
+    acc = s.get_state()[2].sum()
+    assert acc > 0 and np.all(np.isfinite(rows))
+    np.testing.assert_array_equal(s.chi_squared(rows), rows[:, -1])
+    s.close()
+
+
 def test_one_shot_run_gibbs_c_abi(golden, lib_loaded):
     """olpe_run_gibbs (SURVEY.md §8(b)'s one-shot entry point, host buffers in and out)
     called through ctypes as INTEGRATION.md binds it: state, counters and chain equal
