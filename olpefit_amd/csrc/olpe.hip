@@ -150,10 +150,16 @@ template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
 }
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
-// the 2-source 64x64 EXACT sampler's row tables (sweep_exact_rows): [64][4] doubles in
-// the parking area and in the V-table area
-static_assert(WaveSlice<16>::BYTES - WaveSlice<16>::OPE >= 64 * 4 * 8 &&
-              sampler_vtab_bytes(64, 2, 64) >= 64 * 4 * 8, "sweep_exact_rows tables");
+// the EXACT samplers' row tables (sweep_exact_rows, [n][G] doubles each): 64x64 2-source
+// dy in the parking area and c*dy^2 in the V-table area; 64x64 3-source c*dy^2 in the
+// parking area; 32x32 both in the parking area; 128x128 c*dy^2 in the V-table area
+// (the parking area holds the draw tables there)
+template <int NP> constexpr int parking_bytes() { return WaveSlice<NP>::BYTES - WaveSlice<NP>::OPE; }
+static_assert(parking_bytes<16>() >= 64 * 4 * 8 && sampler_vtab_bytes(64, 2, 64) >= 64 * 4 * 8 &&
+              parking_bytes<19>() >= 64 * 6 * 8 && parking_bytes<16>() >= 2 * 32 * 4 * 8 &&
+              parking_bytes<19>() >= 2 * 32 * 6 * 8 && sampler_vtab_bytes(128, 2, 128) >= 128 * 4 * 8 &&
+              sampler_vtab_bytes(128, 3, 128) >= 128 * 6 * 8 && drawtab_extra(32) && drawtab_extra(64),
+              "sweep_exact_rows tables");
 
 __device__ __forceinline__ Trig ld_trig(const double *s) { return Trig{s[0], s[1], s[2]}; }
 __device__ __forceinline__ Coef ld_coef(const double *s) { return Coef{s[0], s[1], s[2]}; }

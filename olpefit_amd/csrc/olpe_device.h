@@ -635,56 +635,70 @@ __device__ __forceinline__ double sweep_exact(const ModelDesc<NSRC> &m, const do
   return acc;
 }
 
-// sweep_exact of the 64x64 EXACT sampler with the row terms from LDS: dy = i - y0 and
-// c*(dy*dy) depend on the row and the Gaussian only, so the wave forms them once per
-// step, lane = row (3 operations per Gaussian for all 64 rows), into ytab / qtab
-// ([64][G] each, LDS the EXACT sampler leaves unused), and each row reads them as
-// wave-uniform broadcasts: 3 operations per pixel and Gaussian for the quadratic form
-// instead of 6, the same operations on the same values, so the same bits.
-template <int NSRC>
+// sweep_exact of the EXACT samplers (n = 32, 64, 128) with row terms from LDS:
+// dy = i - y0 and c*(dy*dy) depend on the row and the Gaussian only, so the wave forms
+// them once per step, lane-parallel over the rows, into qtab (c*dy^2) and, where there is
+// room, ytab (dy) -- [n][G] doubles each, in LDS the EXACT sampler leaves unused -- and
+// the row loop reads them as broadcasts: 3 operations per pixel and Gaussian for the
+// quadratic form instead of 6 (4 without ytab).  The same operations on the same values
+// as sweep_exact, so the same bits (test_exact_sampler_chi2_bitwise_equals_eval).
+template <int NSRC, int NT, bool YT>
 __device__ __forceinline__ double sweep_exact_rows(const ModelDesc<NSRC> &m, const double2 *DE,
                                                    int lane, double *ytab, double *qtab) {
   constexpr int G = 2 * NSRC;
-  {
-    const double yi = (double)lane;
+  constexpr int S = NT >= 64 ? 1 : 64 / NT;      // row groups per wave
+  constexpr int NC = NT >= 64 ? 64 : NT;         // columns per pass
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const double yd = yi - m.g[g].y0;
-      ytab[lane * G + g] = yd;
-      qtab[lane * G + g] = m.g[g].k.c * (yd * yd);
+  for (int r0 = 0; r0 < NT; r0 += 64) {
+    const int r = r0 + lane;
+    if (r < NT) {
+      const double yi = (double)r;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const double yd = yi - m.g[g].y0;
+        if constexpr (YT) ytab[r * G + g] = yd;
+        qtab[r * G + g] = m.g[g].k.c * (yd * yd);
+      }
     }
   }
   wave_sync();
-  const double xj = (double)lane;
-  double t1[G], t2[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const double xd = xj - m.g[g].x0;
-    t1[g] = m.g[g].k.a * (xd * xd);
-    t2[g] = m.g[g].k.b * xd;
-  }
   // the tables' LDS addresses in VGPRs, so that each row's reads are a VGPR base plus
   // immediate offsets (from SGPR bases the compiler copies every address to a VGPR)
   typedef __attribute__((address_space(3))) const double lds_f64;
-  lds_f64 *yl = (lds_f64 *)ytab;
+  lds_f64 *yl = (lds_f64 *)(YT ? ytab : qtab);
   lds_f64 *ql = (lds_f64 *)qtab;
   asm volatile("" : "+v"(yl), "+v"(ql));
+  const int grp = lane / NC, jl = lane - grp * NC;
   double acc = 0.0;
-#pragma unroll 2
-  for (int i = 0; i < 64; ++i) {
-    double v[G];
+#pragma unroll 1
+  for (int c0 = 0; c0 < NT; c0 += 64) {
+    const int j = c0 + jl;
+    const double xj = (double)j;
+    double t1[G], t2[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const double qq = (t1[g] + t2[g] * yl[i * G + g]) + ql[i * G + g];
-      v[g] = m.g[g].amp * exp_neg(qq);
+      const double xd = xj - m.g[g].x0;
+      t1[g] = m.g[g].k.a * (xd * xd);
+      t2[g] = m.g[g].k.b * xd;
     }
-    double mod = v[0] + v[1];
+    // (two rows per trip; one for the 3-source 32x32 sampler, which spills with two)
+#pragma unroll(NSRC == 3 && NT == 32 ? 1 : 2)
+    for (int i = grp; i < NT; i += S) {
+      double v[G];
 #pragma unroll
-    for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
-    mod = mod + m.bg;
-    const double2 de = DE[i * 64 + lane];
-    const double t = (de.x - mod) * de.y;
-    acc = fma(t, t, acc);
+      for (int g = 0; g < G; ++g) {
+        const double yd = YT ? yl[i * G + g] : (double)i - m.g[g].y0;
+        const double qq = (t1[g] + t2[g] * yd) + ql[i * G + g];
+        v[g] = m.g[g].amp * exp_neg(qq);
+      }
+      double mod = v[0] + v[1];
+#pragma unroll
+      for (int s = 1; s < NSRC; ++s) mod = mod + (v[2 * s] + v[2 * s + 1]);
+      mod = mod + m.bg;
+      const double2 de = DE[i * NT + j];
+      const double t = (de.x - mod) * de.y;
+      acc = fma(t, t, acc);
+    }
   }
   wave_sync();   // the tables are rewritten by the next step
   return acc;
@@ -1877,10 +1891,17 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     if (ring) ring->idle_step();
     return part;
   } else {
-    // (the 2-source 64x64 sampler: row tables in its column-term parking area and V
-    // table, both unused in EXACT -- 2 KiB each)
-    if constexpr (NT == 64 && NSRC == 2 && !WRITE) {
-      if (cc) return sweep_exact_rows<NSRC>(m, img, lane, cc->pbuf, vtab);
+    // the EXACT samplers' row tables (olpe.hip checks the sizes): the column-term
+    // parking area (cc->pbuf, NSRC KiB; at n = 128 it holds the draw tables) and the V
+    // table area (vtab), both otherwise unused in EXACT
+    if constexpr (!WRITE && NT == 64 && NSRC == 2) {
+      if (cc) return sweep_exact_rows<NSRC, 64, true>(m, img, lane, cc->pbuf, vtab);
+    } else if constexpr (!WRITE && NT == 64) {
+      if (cc) return sweep_exact_rows<NSRC, 64, false>(m, img, lane, nullptr, cc->pbuf);
+    } else if constexpr (!WRITE && NT == 32) {
+      if (cc) return sweep_exact_rows<NSRC, 32, true>(m, img, lane, cc->pbuf, cc->pbuf + 32 * 2 * NSRC);
+    } else if constexpr (!WRITE && NT == 128) {
+      if (cc) return sweep_exact_rows<NSRC, 128, false>(m, img, lane, nullptr, vtab);
     }
     return sweep_exact<NSRC, NT, WRITE, 2>(m, img, out, n, lane);
   }
