@@ -601,7 +601,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       gcache.same = gmask == 0 && grp == 0;
       // (per-column guard cache: the Gaussians this draw moves or reshapes -- a shape
       // set is the narrow Gaussians, odd g, or the wide ones, even g)
-      gcache.changed = gmask | (grp == 1 ? 0xAAAu : grp == 2 ? 0x555u : 0u) & ((1u << (2 * NSRC)) - 1u);
+      gcache.changed = gmask | ((grp == 1 ? 0xAAAu : grp == 2 ? 0x555u : 0u) & ((1u << (2 * NSRC)) - 1u));
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask, &gcache,
                                                        RING ? &ring : nullptr);
