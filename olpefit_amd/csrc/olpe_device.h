@@ -84,7 +84,7 @@ __device__ __forceinline__ double dpp_f64_any(double v) {
 // 31 and 63 of the last two stages are read, and both lie in the rows those stages
 // write, so the lanes the row masks leave out may hold anything: the moves need no
 // zeroed "old" operand (2 VALU per stage fewer).
-__device__ __forceinline__ double wave_sum(double v) {
+__device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_f64_any<0xB1, 0xf>(v);
   v += dpp_f64_any<0x4E, 0xf>(v);
   v += dpp_f64_any<0x141, 0xf>(v);
@@ -95,6 +95,32 @@ __device__ __forceinline__ double wave_sum(double v) {
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
   return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
+// The same sum on the matrix core: two v_mfma_f64_16x16x4_f64 against a ones matrix.
+// The first takes lane l as A[l & 15][l >> 4] and leaves s_i = sum of lanes i, i+16,
+// i+32, i+48 in rows i of D, lane l holding rows (l >> 4) + 4r in its four result
+// registers (r = 0..3); three adds fold r, so lane l holds t_(l >> 4), and the second
+// MFMA sums the four t over its k dimension into every lane.  8 VALU-port instructions
+// (the ones constant, 2 MFMA, 3 adds, 2 lane reads) where the DPP tree issues 20; the
+// MFMAs run on the matrix core (the sampler does no other matrix work).  Measured 1.5 %
+// slower than the DPP tree on configs[2] (profiles/r02/ab_wavesum_mfma.log): not the
+// default.  A NaN partial propagates (a NaN chi^2 rejects).
+typedef double olpe_v4f64 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double wave_sum_mfma(double v) {
+  const olpe_v4f64 z = {0.0, 0.0, 0.0, 0.0};
+  const olpe_v4f64 d = __builtin_amdgcn_mfma_f64_16x16x4f64(v, 1.0, z, 0, 0, 0);
+  const double t = (d[0] + d[1]) + (d[2] + d[3]);
+  const olpe_v4f64 e = __builtin_amdgcn_mfma_f64_16x16x4f64(t, 1.0, z, 0, 0, 0);
+  return uniform_f64(e[0]);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#ifdef OLPE_WAVESUM_MFMA
+  return wave_sum_mfma(v);       // A/B builds: 1.5 % slower on configs[2]
+#else
+  return wave_sum_dpp(v);
+#endif
 }
 
 // ---------------------------------------------------------------------------------
