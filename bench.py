@@ -56,6 +56,8 @@ CONFIG_NAMES = {
     2: "configs[2]: 65,536 walkers/GPU, 64x64 2-source cutout, fp64, LDS-resident image",
     4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
 }
+# BASELINE.json's metric, character for character (its "64\u00d764")
+METRIC = "walker-steps/sec (= model evals/sec) on 64\u00d764 2-source cutout, 1/2/4/8 GPU"
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
 HBM_PEAK = 8.0e12                 # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # one exp of the EXACT sweep (olpe::exp_neg, ocml's sequence without its range selects):
@@ -348,7 +350,7 @@ def main():
             return out
 
         out = {
-            "metric": "walker-steps/sec (= model evals/sec) on 64x64 2-source cutout, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": value,
             "unit": "walker-steps/s",
             "n_gpus": world,
