@@ -77,7 +77,7 @@ void append_repr(std::string &out, double v) {
     out += '.';
     out.append(digits + 1, (size_t)(nd - 1));
   }
-  char ex[8];
+  char ex[16];
   const int ax = x < 0 ? -x : x;
   snprintf(ex, sizeof(ex), "e%c%02d", x < 0 ? '-' : '+', ax);
   out += ex;
