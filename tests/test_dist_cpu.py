@@ -47,9 +47,10 @@ def _rank_main(rank, world, port, total, n_iters, q):
     g.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multi_rank_sharding_matches_single_process(world):
-    total, n_iters = 5, 60
+@pytest.mark.parametrize("world,total", [(2, 5), (3, 5), (8, 11)])
+def test_multi_rank_sharding_matches_single_process(world, total):
+    # (8 ranks: the configs[3] / SCALE rank count, shards of 1 and 2 walkers)
+    n_iters = 60
     # MASTER_PORT held by another listener, as torchrun's agent store holds it
     taken = socket.socket()
     taken.bind(("127.0.0.1", 0))
