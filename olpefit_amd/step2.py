@@ -17,7 +17,9 @@ reference's files hold at that count, host memory is bounded by one chunk, and a
 checkpoint (walker state, counters, RNG streams, file sizes) after each chunk makes a
 killed run resumable (``--resume``) with the same chains as an uninterrupted one.
 
-Added flags: ``--walkers`` (the reference's MPI size), ``--seed``, ``--iters`` (fixed
+Launched like the reference (``mpiexec -n W python apf_step2.py <image>``), rank 0 runs
+all W walkers and the other ranks exit (``MPI_ENV``).  Added flags: ``--walkers`` (the
+reference's MPI size), ``--seed``, ``--iters`` (fixed
 length instead of accept_min), ``--record-stride``, ``--gpus``, ``--exact``,
 ``--fixed-bkgd``, ``--chunk``, ``--mem-budget``, ``--checkpoint-every``, ``--resume``,
 ``--no-csv``, ``--npy``.
@@ -38,6 +40,28 @@ from .core import Sampler
 
 MAX_CHUNK = 20000          # iterations per launch when memory allows
 
+# The reference is launched as ``mpiexec -n W python apf_step2.py <image>``: one walker
+# per MPI rank.  Launched that way, this build runs all W walkers in
+# rank 0's process on the GPU(s) and the other ranks leave at once, so the same command
+# line gives the same files.  (rank, size) variables of the common launchers:
+MPI_ENV = (("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE"),     # Open MPI
+           ("PMI_RANK", "PMI_SIZE"),                             # MPICH / Intel MPI (Hydra)
+           ("MV2_COMM_WORLD_RANK", "MV2_COMM_WORLD_SIZE"))       # MVAPICH2
+
+
+def mpi_world(environ=None):
+    """(rank, size) of an MPI launch, (0, 1) outside one."""
+    env = os.environ if environ is None else environ
+    for rk, sz in MPI_ENV:
+        if rk in env and sz in env:
+            try:
+                rank, size = int(env[rk]), int(env[sz])
+            except ValueError:
+                continue
+            if size >= 1 and 0 <= rank < size:
+                return rank, size
+    return 0, 1
+
 
 def parse(argv, nsrc, variant="2"):
     prog = {"2": "apf_step2", "2a": "apf_step2a"}[variant] + ("" if nsrc == 2 else "_3body")
@@ -49,8 +73,9 @@ def parse(argv, nsrc, variant="2"):
     if nsrc == 2 and variant == "2":
         ap.add_argument("-i", "--initial_guess_option", type=str,
                         help="-i 1 for the step 1 guess, -i 2a for the step 2a output")
-    ap.add_argument("--walkers", type=int, default=24 if variant == "2" else 1,
-                    help="independent walkers (the reference's MPI processes)")
+    ap.add_argument("--walkers", type=int, default=None if variant == "2" else 1,
+                    help="independent walkers (the reference's MPI processes; default: the "
+                         "size of an mpiexec launch, else 24)")
     ap.add_argument("--accept-min", type=int, default=100000,
                     help="stop when a walker has tried every parameter this often")
     ap.add_argument("--burn-in", type=int,
@@ -81,6 +106,9 @@ def parse(argv, nsrc, variant="2"):
     ap.add_argument("--npy", action="store_true", help="also write {w}_chain.npy")
     ap.add_argument("-q", "--quiet", action="store_true")
     args = ap.parse_args(argv)
+    args.mpi_rank, args.mpi_size = mpi_world() if variant == "2" else (0, 1)
+    if args.walkers is None:
+        args.walkers = args.mpi_size if args.mpi_size > 1 else 24
     if variant == "2a" and args.walkers != 1:
         ap.error("apf_step2a runs one walker (it writes a single step2a.csv)")
     if args.walkers < 1 or args.record_stride < 1 or args.chunk < 0:
@@ -260,6 +288,11 @@ def main(argv=None, nsrc=2, variant="2"):
     (:320-331), which ``apf_step2.py -i 2a`` then starts from (apf_step2.py:248-256)."""
     args = parse(sys.argv[1:] if argv is None else argv, nsrc, variant)
     say = (lambda *a: None) if args.quiet else print
+    if args.mpi_rank > 0:
+        # an mpiexec launch: rank 0 runs every walker (see MPI_ENV)
+        say(f"MPI rank {args.mpi_rank} of {args.mpi_size}: rank 0 runs all "
+            f"{args.walkers} walkers on the GPU; nothing to do here")
+        return pipeline.image_paths(args.image)[2]
     image, hdr = fitsio.getdata_header(args.image)              # apf_step2.py:160-161
     directory, frame, outdir = pipeline.image_paths(args.image)  # :164-170
     say(outdir)

@@ -62,6 +62,25 @@ def test_cli_seeds_are_gpu_count_independent(tmp_path, monkeypatch):
         np.testing.assert_array_equal(np.load(out2 + f"{w}_chain.npy"), one[w])
 
 
+def test_cli_under_mpiexec_equals_walkers_flag(tmp_path, monkeypatch):
+    """``mpiexec -n 3 python apf_step2.py <image>`` (the reference's launch): rank 0 runs
+    the three walkers and writes the same files as ``--walkers 3`` in one process."""
+    for k in [k for pair in step2.MPI_ENV for k in pair]:
+        monkeypatch.delenv(k, raising=False)
+    args = ["--seed", "21", "--iters", "120", "--burn-in", "20", "-q"]
+    path = synth.write_case(str(tmp_path / "a"), 32, 2)
+    out = step2.main([path, "--walkers", "3", *args])
+    path2 = synth.write_case(str(tmp_path / "b"), 32, 2)
+    monkeypatch.setenv("PMI_RANK", "0")
+    monkeypatch.setenv("PMI_SIZE", "3")
+    out2 = step2.main([path2, *args])
+    for w in range(3):
+        for name in (f"{w}_finalarray_mpi.csv", f"{w}_acceptance_rate.csv"):
+            with open(out + name, "rb") as f, open(out2 + name, "rb") as g:
+                assert f.read() == g.read()
+    assert not os.path.exists(out2 + "3_finalarray_mpi.csv")
+
+
 def _oracle_walkers(n, nsrc, seeds, iters):
     from oracle import olpe_oracle as ora
     img, _ = synth.make_image(n, nsrc, 0)

@@ -195,3 +195,26 @@ def test_native_chain_writer_threads(tmp_path):
             assert f.read() == pipeline.format_rows(pipeline.with_seed_row(chains[w]))
     with pytest.raises(OlpeError):
         pipeline.write_chain_csvs([str(tmp_path / "no_dir" / "x.csv")], chains[:1])
+
+
+def test_mpiexec_launch_like_the_reference(tmp_path, monkeypatch):
+    """``mpiexec -n W python apf_step2.py <image>`` (the reference's launch, one walker per
+    rank): --walkers defaults to W, and every rank but 0 leaves before touching the image
+    or the GPU (rank 0 runs all W walkers; its run is the GPU CLI tests' path)."""
+    from olpefit_amd import step2
+    for k in [k for pair in step2.MPI_ENV for k in pair]:
+        monkeypatch.delenv(k, raising=False)
+    assert step2.mpi_world() == (0, 1)
+    assert step2.parse(["a/N2.x.fits"], 2).walkers == 24
+    for rk, sz in step2.MPI_ENV:
+        assert step2.mpi_world({rk: "3", sz: "48"}) == (3, 48)
+    assert step2.mpi_world({"PMI_RANK": "5", "PMI_SIZE": "4"}) == (0, 1)      # inconsistent
+    monkeypatch.setenv("OMPI_COMM_WORLD_RANK", "2")
+    monkeypatch.setenv("OMPI_COMM_WORLD_SIZE", "48")
+    args = step2.parse(["a/N2.x.fits"], 3)
+    assert (args.walkers, args.mpi_rank, args.mpi_size) == (48, 2, 48)
+    assert step2.parse(["a/N2.x.fits", "--walkers", "7"], 2).walkers == 7
+    assert step2.parse(["a/N2.x.fits"], 2, variant="2a").walkers == 1     # 2a: one walker
+    image = str(tmp_path / "N2.20090531.29966.LDIF.fits")                  # never opened
+    out = step2.main([image, "-q"], nsrc=2)
+    assert out == str(tmp_path) + "/29966_apf_results/" and not os.path.exists(out)
