@@ -139,8 +139,17 @@ __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsr
 // 2 x rows x 16 B, which fit in it); the 3-source 64x64 sampler keeps only the shape
 // tables (its V-table fallback runs the exact sweep instead) so that its LDS layout
 // fits 12 waves beside the cutout
-__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt) {
-  return (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
+// The 16-wave 2-source 64x64 FAST sampler keeps ONE shape-table slot (HCache::single:
+// a shape proposal rebuilds its set in place, and after a reject the current state's
+// set is rebuilt at the next step) and has no V-table fallback (its lvl-1 steps take
+// the exact sweep), so that 16 wave slices fit the LDS beside the 64 KiB cutout.
+__host__ __device__ constexpr bool single_h(int nsrc, int nt, int wpb, bool fast) {
+  return nsrc == 2 && nt == 64 && wpb == 16 && fast;
+}
+__host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, int wpb = 12,
+                                                     bool fast = false) {
+  return single_h(nsrc, nt, wpb, fast) ? 64 * 16
+       : (nsrc == 3 && nt == 64) ? 2 * 64 * 16 : ((n * 2 * nsrc * 8 + 15) & ~15);
 }
 // the ring sampler's per-wave slice: the WaveSlice fields up to the parking area, the
 // draw tables there (its sweeps park nothing) and the two FAST3 shape-table slots (no
@@ -274,7 +283,8 @@ void olpe_gibbs_kernel(GibbsArgs A) {
   unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
   double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
   constexpr int TABX = drawtab_extra(NT);
-  const int wstride = RING ? ring_wave_bytes<NP>(n) : WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT);
+  const int wstride = RING ? ring_wave_bytes<NP>(n)
+                           : WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT, WPB, FAST);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (RING ? Ring::BYTES : 0) + (size_t)wave * wstride;
   uint32_t *s_tries = reinterpret_cast<uint32_t *>(wb);
@@ -442,6 +452,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
+    hcache.single = single_h(NSRC, NT, WPB, FAST);
     GuardCache gcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
@@ -854,11 +865,12 @@ template <class T> int dev_alloc(T **p, size_t count) {
 
 // per-wave LDS of the kernel launch_gibbs_m picks: NT = n for LDS images of 32 and 64
 // pixels, otherwise NT = 0 / 128 (no extra draw-table bytes)
-size_t wave_lds(int n, int np, bool lds_img, bool ring = false) {
+size_t wave_lds(int n, int np, bool lds_img, bool ring = false, int wpb = 12,
+                bool fast = false) {
   if (ring) return (size_t)(np == 16 ? ring_wave_bytes<16>(n) : ring_wave_bytes<19>(n));
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
   return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
-         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt);
+         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, wpb, fast);
 }
 
 // Chunks per walker of one launch.  A launch runs W walker chains of n_iters
@@ -901,7 +913,8 @@ int choose_units(long long W, long long slots, long long n_iters, int override_p
 }
 
 size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
-  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring) + kSampHdr;
+  size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring, wpb,
+                                    c->eval_mode == OLPE_EVAL_FAST) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   if (ring) b += wpb >= 12 ? LdsRing<12>::BYTES : LdsRing<6>::BYTES;
   return b;
@@ -975,10 +988,16 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
       case 32: return launch_gibbs_t<NSRC, 32, true, 12, FAST>(c, a);
       case 64: {
         // 12 waves per workgroup (168 VGPRs: four-row update and shape-table prefetch
-        // without spills, 3 waves per SIMD with the walker queue keeping them busy):
-        // FAST +1.7 % over 16, EXACT the same; 16 would not fit the LDS beside the
-        // draw tables' accept thresholds
-        const int wpb = c->wpb ? c->wpb : 12;
+        // without spills, 3 waves per SIMD with the walker queue keeping them busy);
+        // 16 waves (4 per SIMD: the FP64 issue rate of 4 waves, 4.80 against 5.11
+        // cycles per op) for the 2-source FAST sampler when the launch has walkers for
+        // >= 8 rounds of its slots (configs[2]: +1.4 %; with fewer, configs[1]'s 4,096,
+        // the 12-wave sampler's chunked rounds balance better: 16 waves -4.6 %,
+        // profiles/r02/ab_w16.log); it needs the single shape-table slot (single_h), so
+        // EXACT and 3 sources stay at 12
+        int wpb = c->wpb ? c->wpb
+                : (single_h(NSRC, 64, 16, FAST) && a.W >= 8LL * 16 * c->n_cu) ? 16 : 12;
+        if (wpb == 16 && lds_bytes(c, 16) > 160 * 1024) wpb = 12;
         if (wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
         if (wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
         return launch_gibbs_t<NSRC, 64, true, 16, FAST>(c, a);
@@ -1092,7 +1111,8 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     wpb = atoi(e);
     if (wpb != 8 && wpb != 12 && wpb != 16)
       return set_err(OLPE_EINVAL, "OLPE_WPB=%s: must be 8, 12 or 16", e);
-    const size_t b = (size_t)wpb * wave_lds(nx, np_, true) + kSampHdr + npix_ * sizeof(double2);
+    const size_t b = (size_t)wpb * wave_lds(nx, np_, true, false, wpb, true) + kSampHdr +
+                     npix_ * sizeof(double2);
     if (lds_img && nx == 64 && b > 160 * 1024)
       return set_err(OLPE_EINVAL, "OLPE_WPB=%d needs %zu bytes of LDS at %dx%d (%d sources) > 163840",
                      wpb, b, nx, nx, nsrc);

@@ -1173,7 +1173,16 @@ struct HCache {
   bool valid = false;
   int grp = 0;          // this step's proposal: 0 no shape change, 1 narrow set, 2 wide set
   bool flip = false;
+  bool single = false;  // one slot (olpe.hip single_h): a shape proposal rebuilds its set
+                        // in place, so the slot is current only if the proposal is taken
   __device__ __forceinline__ void after(bool accepted) {
+    if (single) {
+      // flip = this step rebuilt the slot in place (FAST3 taken); otherwise the slot
+      // still holds the state before the step
+      if (grp) valid = flip ? accepted : valid && !accepted;
+      flip = false;
+      return;
+    }
     if (accepted && grp) {
       if (flip) cur ^= 1;
       else valid = false;
@@ -1417,10 +1426,12 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // (510 vs 500 M against the 16-wave LEAN one; 3-source 128x128: 88.2 vs 85.7 M).
     // The powers are formed once per column; the recurrence rounds n/RU times down a
     // column.
-    // LEAN: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): two-row
-    // update and no shape-table prefetch; with 12 waves (WIDE, 168 VGPRs) and
-    // elsewhere the four-row update with the prefetch
-    constexpr bool LEAN = (NSRC == 2 && NT == 64 && !WIDE) || (NSRC == 3 && (NT == 64 || NT == 32));
+    // LEAN: the 3-source 32x32 / 64x64 samplers: the two-row update (registers)
+    // W16: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): the
+    // four-row update without the shape-table prefetch (+1.4 % over the 12-wave sampler
+    // on configs[2]; the two-row update ran level with it, profiles/r02/ab_w16.log)
+    constexpr bool W16 = NSRC == 2 && NT == 64 && !WIDE;
+    constexpr bool LEAN = NSRC == 3 && (NT == 64 || NT == 32);
 #ifdef OLPE_ROWU
     constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
 #else
@@ -1429,7 +1440,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 #ifdef OLPE_H_PREFETCH
     constexpr bool HPF = OLPE_H_PREFETCH;
 #else
-    constexpr bool HPF = !LEAN;
+    constexpr bool HPF = !LEAN && !W16;
 #endif
     double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
 #pragma unroll
@@ -1878,6 +1889,13 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
           hc->valid = true;
         }
         h = vtab + hc->cur * tw;
+      } else if (hc->single) {
+        // in place: the proposal's set over the current state's (the other set copied
+        // onto itself); after a reject the slot is marked stale (HCache::after)
+        build_htab<NSRC>(m, vtab, vtab, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3, rows0, kc,
+                         (double)cw.S, lane, ExpTab{etab});
+        hc->flip = true;
+        h = vtab;
       } else {
         double *dst = vtab + (hc->cur ^ 1) * tw;
         build_htab<NSRC>(m, dst, vtab + hc->cur * tw, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3,
@@ -1904,7 +1922,7 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     double part;
     if (lvl == 2) {
       part = sweep_fast2<NSRC, NT, WRITE>(m, img, out, n, lane);
-    } else if (lvl == 1 && !(NSRC == 3 && NT == 64) && !ring) {
+    } else if (lvl == 1 && !(NSRC == 3 && NT == 64) && !ring && !(hc && hc->single)) {
       // (the 3-source 64x64 sampler and the ring sampler have no room for the V table:
       // sampler_vtab_bytes)
       if (hc) hc->valid = false;                           // the V table overwrites vtab

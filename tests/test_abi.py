@@ -86,8 +86,9 @@ def test_null_arguments_are_errors(lib):
 
 def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):
     """OLPE_WPB (a tuning knob) is checked in olpe_create against the 160 KiB LDS before
-    anything touches a GPU: 16 waves of the 64x64 sampler (with its draw tables) do not
-    fit beside the cutout, so the launch would fail; 7 is not a workgroup size."""
+    anything touches a GPU: 16 waves of the 3-source 64x64 sampler do not fit beside the
+    cutout, so the launch would fail (the 2-source FAST one does, with its single
+    shape-table slot); 7 is not a workgroup size."""
     img = np.ones((64, 64), np.float32)
     ctx = C.c_void_p()
 
@@ -95,13 +96,14 @@ def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):
         return lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 64, 64, nsrc,
                                0, 0, C.byref(ctx))
     monkeypatch.setenv("OLPE_WPB", "16")
-    assert create() == _lib.EINVAL
+    assert create(nsrc=3) == _lib.EINVAL
     msg = lib.olpe_last_error().decode()
     assert "bytes of LDS" in msg and int(re.search(r"needs (\d+) bytes", msg).group(1)) > 163840
     monkeypatch.setenv("OLPE_WPB", "7")
     assert create() == _lib.EINVAL and b"8, 12 or 16" in lib.olpe_last_error()
-    monkeypatch.setenv("OLPE_WPB", "12")
     n = C.c_int(0)
     lib.olpe_device_count(C.byref(n))
-    if not n.value:
-        assert create() == _lib.EHIP            # valid knob: fails only for lack of a GPU
+    for wpb in ("12", "16"):
+        monkeypatch.setenv("OLPE_WPB", wpb)
+        if not n.value:
+            assert create() == _lib.EHIP        # valid knob: fails only for lack of a GPU

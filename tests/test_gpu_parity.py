@@ -463,6 +463,23 @@ def _assert_same_run(a, b):
     np.testing.assert_array_equal(a[4], b[4])
 
 
+@pytest.mark.parametrize("units", [0, 3])
+def test_sixteen_wave_sampler_equals_twelve(golden, lib_loaded, monkeypatch, units):
+    """The 2-source 64x64 FAST sampler at 16 waves per workgroup (the default for
+    launches of >= 8 rounds of walkers, e.g. configs[2]; one shape-table slot rebuilt in
+    place, no shape-table prefetch) computes what the 12-wave one does: chains, traces,
+    state, counters and RNG equal bit for bit over launches with odd bounds."""
+    g = golden("c64")
+    W = 4099
+    seeds = 9000 + np.arange(W)
+    runs = []
+    for wpb in ("12", "16"):
+        monkeypatch.setenv("OLPE_WPB", wpb)
+        runs.append(_run_units(g, "fast", W, seeds, units, monkeypatch=monkeypatch, trace=True))
+    _assert_same_run(*runs)
+    assert np.any(runs[0][2][2] > 0)           # some proposals were accepted
+
+
 @pytest.mark.parametrize("units", [0, 2, 3, 7])
 def test_work_units_equal_whole_walkers(golden, lib_loaded, monkeypatch, units):
     """Walkers cut into chunks handed between waves (OLPE_UNITS): 4,099
