@@ -661,13 +661,17 @@ def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
 
 
 @pytest.mark.parametrize("core", [(0.3, 0.3, 0.0), (0.3, 0.5, 0.7), (0.6, 0.45, -0.4)])
-def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core):
+@pytest.mark.parametrize("wpb", ["12", "16"])
+def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core, wpb, monkeypatch):
     """A tiny narrow core (sigma 0.3-0.6 px) fails the FAST3 guard (c S^2 (kc+1)^2 >=
     600), so the sampler's steps take the fallback sweeps inside the 64x64 kernel: the
     V-table (circular core, b = 0) or the exact per-pixel sweep (elongated, rotated
     core), interleaved with FAST3 steps when a proposal widens the core; the shape-table
     cache is invalidated when the V table overwrites it.  3 walkers x 400 iterations
-    against the oracle at the FAST tolerance."""
+    against the oracle at the FAST tolerance.  At 16 waves (one shape-table slot, no V
+    table) the lvl-1 steps take the exact sweep and a rejected shape proposal leaves
+    the slot stale."""
+    monkeypatch.setenv("OLPE_WPB", wpb)
     g = golden("c64")
     dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
     p0 = g["p_init"].copy()
