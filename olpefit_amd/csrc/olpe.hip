@@ -129,9 +129,11 @@ template <int NP> struct WaveSlice {
 // MTWave draw tables (kDrawTab doubles per wave).  Kernels with the FAST3 column-term
 // cache (NT = 32, 64) keep them after the slice; the others in the parking area of
 // the proposal's column terms, which only that cache uses.
+// EXACT samplers keep no accept thresholds (MTWave::thr): kThr doubles
 constexpr int kDrawTabBytes = (kDrawTab * 8 + 15) & ~15;
-__host__ __device__ constexpr int drawtab_extra(int nt) {
-  return (nt != 0 && nt <= 64) ? kDrawTabBytes : 0;
+constexpr int kDrawTabExactBytes = (kThr * 8 + 15) & ~15;
+__host__ __device__ constexpr int drawtab_extra(int nt, bool fast = true) {
+  return (nt != 0 && nt <= 64) ? (fast ? kDrawTabBytes : kDrawTabExactBytes) : 0;
 }
 // bytes of the per-wave V table of sweep_fast: n rows x 2*nsrc doubles
 __host__ __device__ inline int vtab_bytes(int n, int nsrc) { return (n * 2 * nsrc * 8 + 15) & ~15; }
@@ -282,7 +284,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
   double *etab = reinterpret_cast<double *>(smem);
   unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
   double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
-  constexpr int TABX = drawtab_extra(NT);
+  constexpr int TABX = drawtab_extra(NT, FAST);
   const int wstride = RING ? ring_wave_bytes<NP>(n)
                            : WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT, WPB, FAST);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
@@ -426,6 +428,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     mt.has_gauss = ld_uniform(K()->has_gauss + w);
     mt.gauss = uniform_f64(K()->gauss[w]);
     mt.tab = drawtab;
+    mt.thr = FAST;
 
     // accept_min stop (apf_step2.py:300): done_at = the first count at which every
     // parameter has been tried accept_min times.  Touched only when ndone changes (a
@@ -869,8 +872,8 @@ size_t wave_lds(int n, int np, bool lds_img, bool ring = false, int wpb = 12,
                 bool fast = false) {
   if (ring) return (size_t)(np == 16 ? ring_wave_bytes<16>(n) : ring_wave_bytes<19>(n));
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
-  return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) + drawtab_extra(nt) +
-         sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, wpb, fast);
+  return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) +
+         drawtab_extra(nt, fast) + sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, wpb, fast);
 }
 
 // Chunks per walker of one launch.  A launch runs W walker chains of n_iters
@@ -990,13 +993,15 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
         // 12 waves per workgroup (168 VGPRs: four-row update and shape-table prefetch
         // without spills, 3 waves per SIMD with the walker queue keeping them busy);
         // 16 waves (4 per SIMD: the FP64 issue rate of 4 waves, 4.80 against 5.11
-        // cycles per op) for the 2-source FAST sampler when the launch has walkers for
-        // >= 8 rounds of its slots (configs[2]: +1.4 %; with fewer, configs[1]'s 4,096,
-        // the 12-wave sampler's chunked rounds balance better: 16 waves -4.6 %,
-        // profiles/r02/ab_w16.log); it needs the single shape-table slot (single_h), so
-        // EXACT and 3 sources stay at 12
+        // cycles per op) for 2 sources: FAST when the launch has walkers for >= 8 rounds
+        // of its slots (configs[2]: +1.0-1.4 %; with fewer, configs[1]'s 4,096, the
+        // 12-wave sampler's chunked rounds balance better: 16 waves -6 to -10 %), EXACT
+        // always (configs[1]: +19 %, its 4,096 walkers one round of 16-wave slots;
+        // configs[2] level; profiles/r02/ab_w16.log).  The FAST layout needs the single
+        // shape-table slot (single_h), the EXACT one draw tables without the accept
+        // thresholds; 3 sources stay at 12 (their slices do not fit 16)
         int wpb = c->wpb ? c->wpb
-                : (single_h(NSRC, 64, 16, FAST) && a.W >= 8LL * 16 * c->n_cu) ? 16 : 12;
+                : (NSRC == 2 && (!FAST || a.W >= 8LL * 16 * c->n_cu)) ? 16 : 12;
         if (wpb == 16 && lds_bytes(c, 16) > 160 * 1024) wpb = 12;
         if (wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
         if (wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);

@@ -237,6 +237,7 @@ struct MTWave {
   // assembled across the key end; tab[kThr + i] = accept threshold of the rand() at
   // tab[i] (i = 0..63, and 64 for tab[128]): -2 log(u), see accept_threshold
   double *tab;
+  bool thr = true;   // write the accept thresholds (FAST samplers; EXACT has no room)
 
   // load the batch [pos, pos + 64) of the key (at most to its end; a used-up key is
   // twisted first) and prepare its draw tables
@@ -271,7 +272,7 @@ struct MTWave {
     const double f = sqrt(-2.0 * log(r2) / r2);
     tab[lane] = u;
     tab[64 + lane] = ((r2 < 1.0) & (r2 != 0.0)) ? f : -1.0;   // bitwise &: no branches
-    tab[kThr + lane] = accept_threshold(u);
+    if (thr) tab[kThr + lane] = accept_threshold(u);
     wave_sync();
   }
 
@@ -386,7 +387,7 @@ struct MTWave {
           if (lane == 0) {
             const double u = ((double)(w2 >> 5) * 67108864.0 + (double)(w3 >> 6)) / 9007199254740992.0;
             tab[128] = u;
-            tab[kThr + 64] = accept_threshold(u);
+            if (thr) tab[kThr + 64] = accept_threshold(u);
           }
           wave_sync();
           dice_idx = 128;

@@ -463,19 +463,20 @@ def _assert_same_run(a, b):
     np.testing.assert_array_equal(a[4], b[4])
 
 
-@pytest.mark.parametrize("units", [0, 3])
-def test_sixteen_wave_sampler_equals_twelve(golden, lib_loaded, monkeypatch, units):
-    """The 2-source 64x64 FAST sampler at 16 waves per workgroup (the default for
+@pytest.mark.parametrize("mode,units", [("fast", 0), ("fast", 3), ("exact", 0)])
+def test_sixteen_wave_sampler_equals_twelve(golden, lib_loaded, monkeypatch, mode, units):
+    """The 2-source 64x64 samplers at 16 waves per workgroup (FAST: the default for
     launches of >= 8 rounds of walkers, e.g. configs[2]; one shape-table slot rebuilt in
-    place, no shape-table prefetch) computes what the 12-wave one does: chains, traces,
-    state, counters and RNG equal bit for bit over launches with odd bounds."""
+    place, no shape-table prefetch.  EXACT: always; draw tables without the accept
+    thresholds) compute what the 12-wave ones do: chains, traces, state, counters and
+    RNG equal bit for bit over launches with odd bounds."""
     g = golden("c64")
-    W = 4099
+    W = 4099 if mode == "fast" else 1031
     seeds = 9000 + np.arange(W)
     runs = []
     for wpb in ("12", "16"):
         monkeypatch.setenv("OLPE_WPB", wpb)
-        runs.append(_run_units(g, "fast", W, seeds, units, monkeypatch=monkeypatch, trace=True))
+        runs.append(_run_units(g, mode, W, seeds, units, monkeypatch=monkeypatch, trace=True))
     _assert_same_run(*runs)
     assert np.any(runs[0][2][2] > 0)           # some proposals were accepted
 
