@@ -945,7 +945,6 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   q.uflag = c->d_uflag;
   q.utag = 0;
   q.uerr = reinterpret_cast<unsigned *>(c->d_queue + 1);
-  q.balance = c->balance;
   q.stagger = c->stagger;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
@@ -969,6 +968,12 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
     c->utag += 16;
     q.utag = c->utag;
   }
+  // progress balancing (olpe_gibbs_kernel): on by default for a 16-wave 2-source FAST
+  // launch that runs its walkers whole in one round, which ends on its slowest wave
+  // (configs[1]: +2 % over the 12-wave sampler; profiles/r02/ab_w16.log)
+  q.balance = c->balance >= 0 ? c->balance
+            : (LDS && FAST && NSRC == 2 && WPB == 16 && q.units == 1 &&
+               a.W <= (long long)resident * WPB) ? 1 : 0;
   c->last_units = q.units;
   if (q.units > 1) c->units_used = true;
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
@@ -994,14 +999,18 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
         // without spills, 3 waves per SIMD with the walker queue keeping them busy);
         // 16 waves (4 per SIMD: the FP64 issue rate of 4 waves, 4.80 against 5.11
         // cycles per op) for 2 sources: FAST when the launch has walkers for >= 8 rounds
-        // of its slots (configs[2]: +1.0-1.4 %; with fewer, configs[1]'s 4,096, the
-        // 12-wave sampler's chunked rounds balance better: 16 waves -6 to -10 %), EXACT
+        // of its slots (configs[2]: +1.0-1.4 %) or for one round that the 12-wave
+        // sampler cannot hold, run whole with progress balancing (configs[1]'s 4,096:
+        // +2 %; one 12-wave round runs on more CUs: 2,048 walkers -12 % at 16 waves; in
+        // between the 12-wave sampler's chunked rounds balance better), EXACT
         // always (configs[1]: +19 %, its 4,096 walkers one round of 16-wave slots;
         // configs[2] level; profiles/r02/ab_w16.log).  The FAST layout needs the single
         // shape-table slot (single_h), the EXACT one draw tables without the accept
         // thresholds; 3 sources stay at 12 (their slices do not fit 16)
+        const long long r16 = 16LL * c->n_cu, r12 = 12LL * c->n_cu;   // one round
         int wpb = c->wpb ? c->wpb
-                : (NSRC == 2 && (!FAST || a.W >= 8LL * 16 * c->n_cu)) ? 16 : 12;
+                : (NSRC == 2 && (!FAST || a.W >= 8 * r16 || (a.W > r12 && a.W <= r16)))
+                      ? 16 : 12;
         if (wpb == 16 && lds_bytes(c, 16) > 160 * 1024) wpb = 12;
         if (wpb == 8) return launch_gibbs_t<NSRC, 64, true, 8, FAST>(c, a);
         if (wpb == 12) return launch_gibbs_t<NSRC, 64, true, 12, FAST>(c, a);
