@@ -1428,10 +1428,11 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // The powers are formed once per column; the recurrence rounds n/RU times down a
     // column.
     // LEAN: the 3-source 32x32 / 64x64 samplers: the two-row update (registers)
-    // W16: the 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs): the
-    // four-row update without the shape-table prefetch (+1.4 % over the 12-wave sampler
-    // on configs[2]; the two-row update ran level with it, profiles/r02/ab_w16.log)
-    constexpr bool W16 = NSRC == 2 && NT == 64 && !WIDE;
+    // The 2-source 64x64 sampler at 16 waves per workgroup (128 VGPRs) runs the
+    // four-row update with the shape-table prefetch too, at the cost of one 8-byte spill
+    // (stored once per walker): +0.6-1.3 % over it without the prefetch (no spill), which
+    // was +1.0-1.4 % over the 12-wave sampler; the two-row update ran level with 12
+    // waves (profiles/r02/ab_w16.log)
     constexpr bool LEAN = NSRC == 3 && (NT == 64 || NT == 32);
 #ifdef OLPE_ROWU
     constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
@@ -1441,7 +1442,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 #ifdef OLPE_H_PREFETCH
     constexpr bool HPF = OLPE_H_PREFETCH;
 #else
-    constexpr bool HPF = !LEAN && !W16;
+    constexpr bool HPF = !LEAN;
 #endif
     double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
 #pragma unroll

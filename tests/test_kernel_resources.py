@@ -1,10 +1,12 @@
 """Register / scratch budget of the bench sampler kernels (CPU: a device-only hipcc
 compile with the resource-usage remarks, no GPU).
 
-The 64x64 two-source sampler runs 12 waves per workgroup (3 per SIMD), which caps a
-wave at 168 VGPRs; DESIGN.md §3 relies on it having no scratch at all (spilled column
-terms cost the 16-wave variant 0.25 GB of extra HBM writes per launch).  A change that
-makes the FAST or EXACT bench kernel spill fails here before it reaches a GPU.
+The 64x64 two-source sampler runs 12 waves per workgroup (3 per SIMD) for most
+launches, which caps a wave at 168 VGPRs; DESIGN.md §3 relies on it having no scratch
+at all (spilled column terms once cost a 16-wave variant 0.25 GB of extra HBM writes
+per launch).  The 16-wave samplers (configs[2], configs[1]) must fit 128 VGPRs with at
+most the one small spill DESIGN.md §3 accounts for.  A change that breaks either fails
+here before it reaches a GPU.
 
 "No scratch" means no scratch memory instruction in the kernel and no spilled VGPR:
 since the work-unit loop the compiler reserves a 36-B private segment
@@ -72,6 +74,16 @@ def test_bench_sampler_has_no_scratch(usage, fast):
     k = _kernel(usage, 2, 64, True, 12, fast)
     assert k["scratch_insts"] == 0 and k["VGPRs Spill"] == 0, k
     assert k["VGPRs"] <= 168, k
+
+
+def test_sixteen_wave_samplers_fit_four_waves_per_simd(usage):
+    # the configs[2] / configs[1] FAST sampler and the 2-source EXACT one at 16 waves
+    # (DESIGN.md §3): 128 VGPRs at most; FAST keeps the shape-table prefetch at the cost
+    # of one 8-byte spill (one store per walker, three reloads), EXACT spills nothing
+    k = _kernel(usage, 2, 64, True, 16, True)
+    assert k["VGPRs"] <= 128 and k["VGPRs Spill"] <= 2 and 0 <= k["scratch_insts"] <= 4, k
+    k = _kernel(usage, 2, 64, True, 16, False)
+    assert k["VGPRs"] <= 128 and k["VGPRs Spill"] == 0 and k["scratch_insts"] == 0, k
 
 
 def test_other_bench_configs_have_no_scratch(usage):
