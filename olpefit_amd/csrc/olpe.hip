@@ -621,7 +621,9 @@ void olpe_gibbs_kernel(GibbsArgs A) {
                                                        RING ? &ring : nullptr);
       __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
       DT_MARK(3);
-      const double chi = wave_sum(part);
+      // (the total is valid in lane 63: the accept ballots that lane's test, and lane 63
+      // stores an accepted chi^2, so the step needs no readlanes of the sum)
+      const double chi = wave_sum_v(part);
       DT_MARK(4);
 
       // accept_reject (:139-148): EXACT dice < exp(-(chi - cur)/2); FAST the same test
@@ -631,11 +633,21 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       const double la = -dchi / 2.;
       const double dice = drawtab[dice_idx];
       bool acc;
+      uint32_t acc_bit;
       if constexpr (FAST) {
         const double thr = drawtab[kThr + (dice_idx == 128 ? 64 : dice_idx)];
-        acc = __builtin_amdgcn_readfirstlane(dchi < thr ? 1 : 0) != 0;
+        acc_bit = (uint32_t)(__builtin_amdgcn_ballot_w64(dchi < thr) >> 32) >> 31;
       } else {
-        acc = __builtin_amdgcn_readfirstlane(dice < exp(la) ? 1 : 0) != 0;
+        acc_bit = (uint32_t)(__builtin_amdgcn_ballot_w64(dice < exp(la)) >> 32) >> 31;
+      }
+      asm volatile("" : "+s"(acc_bit));     // (kept a scalar: no VALU compare of the ballot)
+      acc = acc_bit != 0;
+      if (acc && lane == 63) st[PS - 1] = chi;
+      // (the trace's uniform copies, taken here so that the sum's VGPRs die at the store)
+      double chi_u = 0.0, la_u = 0.0;
+      if (A.trace) {
+        chi_u = lane63_f64(chi);
+        la_u = lane63_f64(la);
       }
       hcache.after(acc);
       gcache.after(acc);
@@ -649,7 +661,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       if (acc && lane == 0) {
         s_acc[r] = s_acc[r] + 1u;
         st[r] = nv;
-        st[PS - 1] = chi;
         if (grp) {
           double *dt = st + (grp == 1 ? WS::OT1 : WS::OT2);
           double *dc = st + (grp == 1 ? WS::OC1 : WS::OC2);
@@ -661,14 +672,16 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       DT_MARK(5);
 
 #if !defined(OLPE_DIAG_TIMING) && !defined(OLPE_DIAG_SPAN)
-      if (A.trace && lane == 0) {
+      if (A.trace) {
+       if (lane == 0) {
         double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
         t[0] = (double)r;
         t[1] = nv;
-        t[2] = chi;
+        t[2] = chi_u;
         t[3] = dice;
-        t[4] = FAST ? (la == la ? ExpTab{etab}(la) : la) : exp(la);   // p_accept
+        t[4] = FAST ? (la_u == la_u ? ExpTab{etab}(la_u) : la_u) : exp(la_u);   // p_accept
         t[5] = acc ? 1.0 : 0.0;
+       }
       }
 #endif
       // chain record (:342-351, generalised to a stride)

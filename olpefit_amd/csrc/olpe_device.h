@@ -84,18 +84,24 @@ __device__ __forceinline__ double dpp_f64_any(double v) {
 // 31 and 63 of the last two stages are read, and both lie in the rows those stages
 // write, so the lanes the row masks leave out may hold anything: the moves need no
 // zeroed "old" operand (2 VALU per stage fewer).
-__device__ __forceinline__ double wave_sum_dpp(double v) {
+// The tree without the broadcast: the total is valid in lane 63 only (a caller that
+// only tests it, e.g. the accept, ballots lane 63 and skips the two readlanes).
+__device__ __forceinline__ double wave_sum_dpp_v(double v) {
   v += dpp_f64_any<0xB1, 0xf>(v);
   v += dpp_f64_any<0x4E, 0xf>(v);
   v += dpp_f64_any<0x141, 0xf>(v);
   v += dpp_f64_any<0x140, 0xf>(v);
   v += dpp_f64_any<0x142, 0xa>(v);
   v += dpp_f64_any<0x143, 0xc>(v);
+  return v;
+}
+__device__ __forceinline__ double lane63_f64(double v) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
   return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
 }
+__device__ __forceinline__ double wave_sum_dpp(double v) { return lane63_f64(wave_sum_dpp_v(v)); }
 
 // The same sum on the matrix core: two v_mfma_f64_16x16x4_f64 against a ones matrix.
 // The first takes lane l as A[l & 15][l >> 4] and leaves s_i = sum of lanes i, i+16,
@@ -120,6 +126,14 @@ __device__ __forceinline__ double wave_sum(double v) {
   return wave_sum_mfma(v);       // A/B builds: 1.5 % slower on configs[2]
 #else
   return wave_sum_dpp(v);
+#endif
+}
+// the wave sum valid in lane 63 (every lane for the MFMA form)
+__device__ __forceinline__ double wave_sum_v(double v) {
+#ifdef OLPE_WAVESUM_MFMA
+  return wave_sum_mfma(v);
+#else
+  return wave_sum_dpp_v(v);
 #endif
 }
 
@@ -1171,17 +1185,19 @@ struct GuardCache {
 
 struct HCache {
   int cur = 0;
-  bool valid = false;
+  int valid = 0;        // (ints, not bools: a uniform bool carried across the sampler
+                        // loop is kept as a lane mask, read back with v_cndmask +
+                        // v_readfirstlane)
   int grp = 0;          // this step's proposal: 0 no shape change, 1 narrow set, 2 wide set
-  bool flip = false;
-  bool single = false;  // one slot (olpe.hip single_h): a shape proposal rebuilds its set
+  int flip = 0;
+  int single = 0;       // one slot (olpe.hip single_h): a shape proposal rebuilds its set
                         // in place, so the slot is current only if the proposal is taken
   __device__ __forceinline__ void after(bool accepted) {
     if (single) {
       // flip = this step rebuilt the slot in place (FAST3 taken); otherwise the slot
       // still holds the state before the step
-      if (grp) valid = flip ? accepted : valid && !accepted;
-      flip = false;
+      if (grp) valid = flip ? (int)accepted : valid & (int)!accepted;
+      flip = 0;
       return;
     }
     if (accepted && grp) {
