@@ -494,7 +494,8 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       DT_MARK(0);
 
       // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
-      const double cur = uniform_f64(st[r]);
+      // (read by every lane: nv is made uniform below, cur needs no readfirstlane)
+      const double cur = st[r];
       const double wr = width_of<NSRC>(r);
       double nv;
       if ((L::LOGMASK >> r) & 1u) {
