@@ -45,7 +45,12 @@ def _dptr(a):
 def noise_model(image, itime, coadds, multisam, sampmode):
     """apf_step2.py:176-210: (mask, pois2, readnoise2, satlevel, readnoise).
 
-    ``mask`` = ``np.ma.masked_greater(image, 0.8*satlevel)``'s mask;
+    ``mask`` = ``np.ma.masked_greater(image, 0.8*satlevel)``'s mask (:188) together with
+    every pixel whose residual the reference's ``np.ma`` arithmetic drops in
+    ``chi_squared`` (:134-137): ``np.ma.divide`` masks a non-finite quotient and a zero
+    divisor, so a NaN or -inf data pixel, and a pixel whose ``err`` is NaN or 0, never
+    enters chi^2 (+inf is already above the saturation level).  olpe_create applies the
+    same rule to what it is given.
     ``pois2`` = ``np.sqrt(np.abs(image))**2`` in the image dtype (float32 for BITPIX
     -32, as the reference rounds it); ``readnoise2`` = ``readnoise**2``."""
     itime = float(itime) * 1000.
@@ -61,7 +66,10 @@ def noise_model(image, itime, coadds, multisam, sampmode):
     else:
         readnoise = 38 * (np.sqrt(coadds))
     rn = np.float64(readnoise)
-    pois2 = np.sqrt(np.abs(image)) ** 2
+    with np.errstate(invalid="ignore"):
+        pois2 = np.sqrt(np.abs(image)) ** 2
+        err = np.sqrt(rn * rn + pois2.astype(np.float64))          # :210
+        mask = mask | ~np.isfinite(image) | ~np.isfinite(err) | (err == 0)
     return mask, pois2, float(rn * rn), satlevel, float(readnoise)
 
 

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <vector>
 
@@ -1075,6 +1076,7 @@ int ensure_ensemble(olpe_ctx *c, int W) {
   c->seeded = false;
   c->count = 0;
   c->chain_rows = 0;
+  c->mom_n = 0;
   return OLPE_OK;
 }
 
@@ -1171,7 +1173,11 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     const double p2 = image_dtype == OLPE_DTYPE_F32 ? (double)((const float *)pois2)[i]
                                                     : ((const double *)pois2)[i];
     const double e = sqrt(readnoise2 + p2);   // apf_step2.py:210
-    if (mask && mask[i]) {
+    // the reference's np.ma chi_squared (:134-137) drops a pixel whose quotient
+    // (D - M) / err is non-finite or whose err is 0 (np.ma.divide's domain): a NaN or
+    // -inf data pixel, or an err that is NaN or 0 (+inf data is above the saturation
+    // mask of :188 already).  Staged {0, 0}, such a pixel adds nothing to chi^2.
+    if ((mask && mask[i]) || !std::isfinite(d) || !(e > 0.0)) {
       hDE[i] = make_double2(0.0, 0.0);
       hDW[i] = make_double2(0.0, 0.0);
     } else {
@@ -1239,7 +1245,7 @@ void olpe_destroy(olpe_ctx *c) {
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue,
-                  c->d_gather, c->d_uflag};
+                  c->d_gather, c->d_uflag, c->d_mmean, c->d_mm2, c->d_mpart};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &pair : c->ev)
@@ -1317,6 +1323,8 @@ int olpe_seed(olpe_ctx *c, const uint32_t *seeds, int W) {
   HIPCHK(hipStreamSynchronize(c->stream));
   (void)hipFree(ds);
   c->seeded = true;
+  c->mom_n = 0;                  // a new run: no rows folded into the moments yet
+  c->mom_folded = c->launches;
   return OLPE_OK;
 }
 

@@ -151,9 +151,26 @@ def param_cases(n, nsrc, p_init, rs):
     return np.array(cases)
 
 
-def make_case(name, n, nsrc, n_walkers, accept_min, burn_in, n_model=None):
+def bad_pixels(n, nsrc):
+    """Non-finite data pixels (row, col, value) for the ``*_nan`` cases: NaN and -inf
+    in the star's wing (below the saturation mask), by the companion and in the sky,
+    and one +inf (already masked by masked_greater, apf_step2.py:188).  The pixels the
+    initial guess reads (amplitudes, apf_step2.py:267-268; sky box, :269-271) stay
+    finite."""
+    g = synth.guess_values(n, nsrc)
+    rs, cs = int(g[1] - 1), int(g[0] - 1)
+    rc, cc = int(g[3] - 1), int(g[2] - 1)
+    return [(rs - 2, cs - 1, np.nan), (rs - 2, cs + 2, -np.inf), (rc + 1, cc + 1, np.nan),
+            (rc - 1, cc, -np.inf), (n - 3, n - 5, -np.inf), (n // 2 + 6, 4, np.nan),
+            (n - 2, 3, np.inf)]
+
+
+def make_case(name, n, nsrc, n_walkers, accept_min, burn_in, n_model=None, nonfinite=False):
     spec = TWO if nsrc == 2 else THREE
     image, _ = synth.make_image(n, nsrc, seed=0)
+    if nonfinite:
+        for r, c, v in bad_pixels(n, nsrc):
+            image[r, c] = v
     image = image.astype(">f4")                  # what fits.open returns for BITPIX -32
     header = dict((k.lower(), v) for k, v in synth.HEADER.items())
     guess = synth.guess_values(n, nsrc)
@@ -258,6 +275,12 @@ def make_fits():
 
 if __name__ == "__main__":
     np.seterr(all="ignore")
+    if sys.argv[1:] == ["nonfinite"]:
+        # round 3: cutouts with NaN / -inf / +inf data pixels (the reference's np.ma
+        # chi_squared drops them, apf_step2.py:134-137 on the array from :188)
+        make_case("c32_nan", 32, 2, n_walkers=3, accept_min=40, burn_in=5, nonfinite=True)
+        make_case("c64_nan", 64, 2, n_walkers=2, accept_min=30, burn_in=5, nonfinite=True)
+        sys.exit(0)
     make_rng()
     make_fits()
     make_case("c32", 32, 2, n_walkers=4, accept_min=40, burn_in=5)

@@ -24,7 +24,9 @@ from oracle import olpe_oracle as ora
 
 pytestmark = pytest.mark.gpu
 
-CASES = ["c32", "c64", "c64_3", "c128_3"]
+# *_nan: NaN / -inf / +inf data pixels, dropped by the reference's np.ma chi_squared
+# (apf_step2.py:134-137; fixtures from make_golden.py ``nonfinite``)
+CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan"]
 
 
 def make_sampler(g, mode="exact", **kw):
@@ -141,6 +143,21 @@ def test_trajectories_match_reference(golden, lib_loaded, name, mode):
         _check_traj(tr, g, w, Lw, name, TOL[mode]["traj"])
         np.testing.assert_allclose(chain[w, :Lw], g["traj_params"][w, :Lw],
                                    rtol=TOL[mode]["traj"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name", ["c32_nan", "c64_nan"])
+def test_nonfinite_pixels_dropped_by_the_library(golden, lib_loaded, name, mode):
+    """olpe_create drops NaN / -inf data pixels by itself: given only the reference's
+    saturation mask (np.ma.masked_greater, apf_step2.py:188), which does not cover them,
+    chi^2 still equals the reference's finite values."""
+    from olpefit_amd.core import Sampler
+    g = golden(name)
+    s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=2, mask=g["mask"])
+    s.set_eval_mode(mode)
+    chi = s.chi_squared(g["params"])
+    assert np.all(np.isfinite(chi))
+    np.testing.assert_allclose(chi, g["chi2"], rtol=TOL[mode]["chi"])
 
 
 @pytest.mark.parametrize("name", ["c32", "c64_3"])

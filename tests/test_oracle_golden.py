@@ -13,7 +13,9 @@ import pytest
 from oracle import olpe_oracle as ora
 from oracle.legacy_rng import LegacyMT
 
-CASES = ["c32", "c64", "c64_3", "c128_3"]
+# *_nan: the c32 / c64 cutouts with NaN, -inf and +inf data pixels (make_golden.py
+# ``nonfinite``): the reference's np.ma chi_squared drops them (apf_step2.py:134-137)
+CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan"]
 
 
 def test_rng_numpy_stream_frozen(golden):
@@ -56,7 +58,7 @@ def test_noise_model_and_init(golden, name):
     nsrc = int(g["nsrc"])
     dm, err, sat, rn = ora.noise_model(img, 1.0, 1, 1, 2)
     assert np.array_equal(np.ma.getmaskarray(dm), g["mask"])
-    assert np.array_equal(err, g["err"])
+    assert np.array_equal(err, g["err"], equal_nan=True)
     assert sat == g["satlevel"] and rn == g["readnoise"]
     p0 = ora.initial_parameters(img, g["guess"], nsrc)
     assert np.array_equal(p0[:-1], g["p_init"][:-1])
@@ -99,3 +101,24 @@ def test_trajectories(golden, name):
             np.testing.assert_allclose(new, g["traj_new"][w, i], rtol=1e-12)
             np.testing.assert_allclose(chi, g["traj_chi"][w, i], rtol=1e-12)
             np.testing.assert_allclose(walker.parameters, g["traj_params"][w, i], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["c32_nan", "c64_nan"])
+def test_nonfinite_pixels_drop_out(golden, name):
+    """The fixture's chi^2 values are finite and equal the sum over the pixels that are
+    neither saturation-masked nor non-finite in D or err -- the mask the product stages
+    (core.noise_model + olpe_create)."""
+    from olpefit_amd.core import noise_model
+    g = golden(name)
+    img = g["image"]
+    n = img.shape[0]
+    assert not np.all(np.isfinite(img))
+    mask, pois2, rn2, _, _ = noise_model(img, 1.0, 1, 1, 2)
+    err = np.sqrt(rn2 + pois2.astype(np.float64))
+    assert np.array_equal(mask, g["mask"] | ~np.isfinite(img) | ~np.isfinite(err))
+    keep = ~mask
+    for k, p in enumerate(g["params"][:6]):
+        m = ora.build_analytical_model(p, n, 2)
+        chi = np.sum(((img.astype(np.float64)[keep] - m[keep]) / err[keep]) ** 2)
+        assert np.isfinite(g["chi2"][k])
+        np.testing.assert_allclose(chi, g["chi2"][k], rtol=1e-12)
