@@ -170,7 +170,8 @@ def cpu_baseline(n: int, nsrc: int, total_iters: int):
 
 def _comm_timeout(rank: int, make_report, timeout: float):
     """Watchdog of the end-of-run RCCL exchange: rank 0 prints the measurement with the
-    error, then every rank leaves (os._exit: the hung collective never returns)."""
+    error, then every rank leaves with status 3 (os._exit: the hung collective never
+    returns; the launcher and CI see the failure, the JSON line keeps the numbers)."""
     print(f"[bench rank {rank}] RCCL exchange still running after {timeout:g} s: giving up",
           file=sys.stderr)
     if rank == 0:
@@ -178,7 +179,7 @@ def _comm_timeout(rank: int, make_report, timeout: float):
         out["comm_error"] = f"TimeoutError: RCCL exchange did not finish within {timeout:g} s"
         print(json.dumps(out), flush=True)
     sys.stderr.flush()
-    os._exit(0)
+    os._exit(3)
 
 
 def load_json(path: str):
@@ -216,6 +217,14 @@ def main():
     ap.add_argument("--comm-timeout", type=float, default=240.0,
                     help="N > 1: seconds the end-of-run RCCL exchange may take before rank 0 "
                          "reports the measurement without it")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the end-of-run RCCL exchange (state and chain all-gather, "
+                         "moments all-reduce) even with one rank (a one-rank communicator)")
+    ap.add_argument("--verify-exchange", action="store_true",
+                    help="also gather every range into host memory and check that this "
+                         "rank's block equals its own chain rows (exchange_verified)")
+    ap.add_argument("--no-moments", action="store_true",
+                    help="do not fold each launch's rows into the device moments")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0, no RCCL "
                          "all-gather (RCCL refuses two ranks on one device)")
@@ -261,6 +270,8 @@ def main():
         s.set_eval_mode(mode)
         for _ in range(warmup):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+            if not args.no_moments:
+                s.moments_accumulate()
         s.sync()
         barrier()
         s.sync()
@@ -268,6 +279,11 @@ def main():
         kms = []
         for i in range(steps):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
+            if not args.no_moments:
+                # the launch's rows into the whole-run posterior moments (a separate,
+                # HBM-bound kernel on the same stream: inside the timed step, outside
+                # the sampler's kernel_ms)
+                s.moments_accumulate()
             if (i + 1) % 64 == 0:                # the event ring holds 64 launches
                 kms.extend(s.kernel_times(64))
         s.sync()
@@ -322,6 +338,14 @@ def main():
                     valu_per_walker_step=vc["valu_per_step"],
                     valu_issue_frac=rate * vc["valu_per_step"] * 64 / FP64_LANE_PEAK,
                     counts_stale=vc.get("kernel_digest") != digest)
+                prof = vc.get("profile")
+                if prof:
+                    # the profiling session the counts come from (tools/roofline_session.sh):
+                    # its rocprofv3 kernel time, HIP-event time and clock, and the frac
+                    # they give -- reproducible from the committed profiles/ files; this
+                    # line's frac differs from it by this box's speed (kernel_ms ratio)
+                    out["profile"] = dict(prof, frac_ratio_live_over_profile=(
+                        prof["rocprof_kernel_ms"] / kernel_ms))
             else:                       # no counters for this shape: the model's own count
                 ops = work_per_step(n, nsrc, mode)
                 out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
@@ -387,12 +411,13 @@ def main():
     # recorded in the JSON line instead of losing the measurement.
     comm = {}
     watchdog = None
+    moments = None
 
     def watchdog_cancel():
         if watchdog is not None:
             watchdog.cancel()
 
-    if world > 1 and not args.share_gpu:
+    if (world > 1 or args.exchange) and not args.share_gpu:
         # watchdog: a hung exchange (never observed; RCCL init or a collective waiting on
         # a lost peer) must not cost the measurement -- rank 0 prints its line with the
         # error after --comm-timeout s and every rank exits
@@ -410,6 +435,12 @@ def main():
             comm["allgather_ms"] = allmax(time.perf_counter() - tg) * 1e3
             if allst.shape != (world * wpg, s.ps):
                 raise RuntimeError(f"all-gather returned {allst.shape}")
+            if not np.array_equal(allst[rank * wpg:(rank + 1) * wpg], s.get_state()[0]):
+                raise RuntimeError("all-gathered states differ from this rank's")
+            if not args.no_moments:
+                tm = time.perf_counter()
+                moments = s.allreduce_moments()               # over every rank's walkers
+                comm["moments_allreduce_ms"] = allmax(time.perf_counter() - tm) * 1e3
             per_walker = s._nrec * s.ps * 8
             wn = max(1, min(wpg, int(args.gather_mib * 2 ** 20 // max(1, per_walker))))
             s.allgather_chain(0, min(wn, wpg), out=False)         # warm-up (buffer, rings)
@@ -421,7 +452,19 @@ def main():
             nbytes = world * wpg * per_walker
             comm.update(chain_gather_ms=t * 1e3, chain_gather_bytes=nbytes,
                         chain_gather_ranges=(wpg + wn - 1) // wn,
-                        chain_gather_gbs=nbytes * (world - 1) / world / t / 1e9)
+                        chain_gather_range_walkers=min(wn, wpg),
+                        chain_gather_gbs=nbytes * (world - 1) / world / t / 1e9
+                        if world > 1 else None)
+            if args.verify_exchange:
+                # every range into host memory: this rank's block must be its own rows
+                local = s.chain()
+                for w0 in range(0, wpg, wn):
+                    got = s.allgather_chain(w0, min(wn, wpg - w0))
+                    if got.shape[0] != world or not np.array_equal(got[rank],
+                                                                   local[w0:w0 + wn]):
+                        raise RuntimeError(f"gathered range [{w0}, {w0 + wn}) differs from "
+                                           f"rank {rank}'s chain")
+                comm["exchange_verified"] = True
         except Exception as e:          # noqa: BLE001 -- reported, not hidden
             comm["comm_error"] = f"{type(e).__name__}: {e}"
             print(f"[bench rank {rank}] RCCL exchange failed: {comm['comm_error']}",
@@ -435,6 +478,21 @@ def main():
 
     watchdog_cancel()
     out = report(elapsed, kernel_ms, units, acceptance, comm, alt)
+    if moments is None and world == 1 and not args.exchange and not args.no_moments:
+        moments = s.allreduce_moments()          # no communicator: this context alone
+    if moments is not None:
+        # step 3's posterior statistics from the whole-run device moments (every timed and
+        # warm-up launch of every rank), without a chain read
+        from olpefit_amd import step3
+        summ = step3.summary_from_moments(moments, nsrc)
+        names = step3.NAMES_2 if nsrc == 2 else step3.NAMES_3
+        out["posterior"] = {
+            "rows_per_walker": summ["_rows_per_walker"], "walkers": summ["_walkers"],
+            "means": {k: summ[k]["mean"] for k in names[:4]},
+            "stds": {k: summ[k]["std"] for k in names[:4]},
+            "gr_rc_max": max(summ[k]["gr_rc"] for k in names[:-1]),
+            "acceptance": sum(summ[k]["accepts"] for k in names[:-1])
+            / sum(summ[k]["tries"] for k in names[:-1])}
     value = out["value"]
     if not args.no_cpu_baseline and world == 1:
         cpu_steps = args.cpu_steps or max(4000, 96000 * 64 * 64 // (n * n))

@@ -178,6 +178,18 @@ int olpe_csv_append_chains(const char *const *paths, const double *chains, int n
                            long long rows_per_file, long long nrows, int ncols, int threads,
                            long long *sizes_out);
 
+/* Step 3's read of the same files (apf_step3.py:169-186: np.genfromtxt per walker
+ * file, the walkers collated as columns).  olpe_csv_shape: *rows = non-blank lines,
+ * *cols = fields of the first line (step 3 takes the length from walker 0's file).
+ * olpe_csv_read_chains: nfiles files of nrows x ncols each, rows [skip, nrows) into
+ * out[nrows - skip][nfiles][ncols] (skip = step 3's additional_burnin, :190-205), parsed
+ * from `threads` threads (0 = one per core); values equal genfromtxt's bit for bit
+ * (correctly rounded; empty field = NaN).  A file of another shape is OLPE_EINVAL
+ * naming the file (the reference fails assigning it into its [length, ncor] arrays). */
+int olpe_csv_shape(const char *path, long long *rows, int *cols);
+int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, int ncols,
+                         long long skip, double *out, int threads);
+
 /* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
 int olpe_comm_unique_id(uint8_t *id128);
@@ -196,10 +208,42 @@ int olpe_comm_allgather_state(olpe_ctx *ctx, double *out);
  * OLPE_EINVAL on every rank otherwise). */
 int olpe_comm_allgather_chain(olpe_ctx *ctx, long long w0, long long wn, double *out,
                               long long *nrec_out);
-/* All-reduce per-parameter moments of the last launch's chain (or of the final
- * states when no chain was recorded): out[3*PS] = {n, sum[PS], sumsq[PS]} with n
- * repeated in slot 0 of the first block, see DESIGN.md §6. */
+/* Posterior summary over every rank from the whole-run moments (olpe_moments_*): two
+ * all-reduces (sum), the pooled mean first, then the deviations of the walkers' means
+ * about it.  out[OLPE_MOMENTS_LEN(PS, P)] as for olpe_moments_summary, over all ranks'
+ * walkers, with centre = the pooled mean (out[2 + k] / out[1]).  Every rank must have
+ * folded the same number of rows (checked: OLPE_EINVAL on every rank otherwise).
+ * Without olpe_comm_init it summarises this context alone. */
 int olpe_comm_allreduce_moments(olpe_ctx *ctx, double *out);
+
+/* --- whole-run posterior moments ----------------------------
+ * apf_step3.py reads every chain file (:169-186) to compute per-parameter means, sigmas
+ * and the Gelman-Rubin PSRF / RC (:258-278).  Those need, per walker w and column k,
+ * only the walker's mean and sum of squared deviations M2 over its rows, which the
+ * device keeps for every row the walker recorded: the summary then needs neither the
+ * chain files nor a chain gather.  Rows = what the chain files hold after step 3's
+ * default additional_burnin = 1 (the NaN seed row) -- every recorded row. */
+/* Fold the last launch's recorded rows into the running (mean, M2) of every walker and
+ * column (async; once per launch: OLPE_ESTATE if this launch was folded already).
+ * olpe_seed starts a new run (no rows folded). */
+int olpe_moments_accumulate(olpe_ctx *ctx);
+int olpe_moments_reset(olpe_ctx *ctx);
+/* *n = rows folded per walker; mean / m2 [W][PS] (either may be NULL).  _set restores a
+ * checkpoint (n = 0: nothing folded; mean / m2 may then be NULL). */
+int olpe_moments_get(olpe_ctx *ctx, long long *n, double *mean, double *m2);
+int olpe_moments_set(olpe_ctx *ctx, long long n, const double *mean, const double *m2);
+/* Per-column sums over this context's walkers (no communication):
+ *   out[0] = n rows per walker, out[1] = walkers W,
+ *   out[2 + k]          = sum_w mean_w[k]                         (k < PS)
+ *   out[2 + PS + k]     = sum_w M2_w[k]
+ *   out[2 + 2*PS + k]   = sum_w (mean_w[k] - centre[k])^2         (0 if centre is NULL)
+ *   out[2 + 3*PS + j]   = sum_w tries_w[j], out[2 + 3*PS + P + j] = sum_w accepts_w[j]
+ *                                                                 (j < P, whole run)
+ * Per-parameter mean = out[2+k] / W; step 3's np.std over all rows =
+ * sqrt((out[2+PS+k] + n * out[2+2PS+k]) / (n W)) with centre = that mean; GR's within
+ * term = out[2+PS+k] / (n W), its between sum = out[2+2PS+k] (step3.summary_from_moments). */
+#define OLPE_MOMENTS_LEN(ps, np) (2 + 3 * (ps) + 2 * (np))
+int olpe_moments_summary(olpe_ctx *ctx, const double *centre, double *out);
 
 #ifdef __cplusplus
 }

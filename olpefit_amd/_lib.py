@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OLPE_LIB", os.path.join(HERE, "libolpe.so"))
 
-OK, EINVAL, EHIP, ENOMEM, ESTATE, ECOMM = 0, -1, -2, -3, -4, -5
+OK, EINVAL, EHIP, ENOMEM, ESTATE, ECOMM, EIO = 0, -1, -2, -3, -4, -5, -6
 DTYPE_F32, DTYPE_F64 = 0, 1
 EVAL_EXACT, EVAL_FAST = 0, 1
 
@@ -66,6 +66,13 @@ SIGNATURES = {
                              C.POINTER(C.c_size_t)]),
     "olpe_csv_write_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _i, _i, _i]),
     "olpe_csv_append_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _ll, _i, _i, _pll]),
+    "olpe_csv_shape": (_i, [C.c_char_p, _pll, C.POINTER(_i)]),
+    "olpe_csv_read_chains": (_i, [C.POINTER(C.c_char_p), _i, _ll, _i, _ll, _pd, _i]),
+    "olpe_moments_accumulate": (_i, [_P]),
+    "olpe_moments_reset": (_i, [_P]),
+    "olpe_moments_get": (_i, [_P, _pll, _pd, _pd]),
+    "olpe_moments_set": (_i, [_P, _ll, _pd, _pd]),
+    "olpe_moments_summary": (_i, [_P, _pd, _pd]),
     "olpe_comm_unique_id": (_i, [_pu8]),
     "olpe_comm_init": (_i, [_P, _pu8, _i, _i]),
     "olpe_comm_allgather_state": (_i, [_P, _pd]),

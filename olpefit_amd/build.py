@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libolpe.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("olpe.hip", "olpe_comm.hip", "olpe_csv.cpp")]
+SOURCES = [os.path.join(CSRC, f) for f in ("olpe.hip", "olpe_comm.hip", "olpe_moments.hip", "olpe_csv.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("olpe_device.h", "olpe_internal.h",
                                                  "exp_table.h")] + [
     os.path.join(REPO, "include", "olpe.h")]

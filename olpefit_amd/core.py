@@ -295,6 +295,42 @@ class Sampler:
         return buf
 
     def allreduce_moments(self):
-        out = np.empty(1 + 2 * self.ps)
+        """Posterior sums over every rank's walkers (olpe_comm_allreduce_moments; this
+        context alone without comm_init): the olpe_moments_summary layout with the
+        centre at the pooled mean -- see ``step3.summary_from_moments``."""
+        out = np.empty(self.moments_len)
         check(self._lib.olpe_comm_allreduce_moments(self._ctx, _dptr(out)))
+        return out
+
+    # -- whole-run moments (SURVEY.md §8(f) row 1) ---------------------------------
+    @property
+    def moments_len(self) -> int:
+        return 2 + 3 * self.ps + 2 * self.np_           # OLPE_MOMENTS_LEN(PS, P)
+
+    def moments_accumulate(self):
+        """Fold the last launch's recorded rows into every walker's running (mean, M2)
+        (async, on the device; once per launch)."""
+        check(self._lib.olpe_moments_accumulate(self._ctx))
+
+    def moments_reset(self):
+        check(self._lib.olpe_moments_reset(self._ctx))
+
+    def moments(self):
+        """(n rows per walker, mean [W, PS], M2 [W, PS])."""
+        n = C.c_longlong(0)
+        mean = np.empty((self.W, self.ps))
+        m2 = np.empty((self.W, self.ps))
+        check(self._lib.olpe_moments_get(self._ctx, C.byref(n), _dptr(mean), _dptr(m2)))
+        return int(n.value), mean, m2
+
+    def set_moments(self, n, mean=None, m2=None):
+        mean = None if mean is None else np.ascontiguousarray(mean, dtype=np.float64)
+        m2 = None if m2 is None else np.ascontiguousarray(m2, dtype=np.float64)
+        check(self._lib.olpe_moments_set(self._ctx, int(n), _dptr(mean), _dptr(m2)))
+
+    def moments_summary(self, centre=None):
+        """Per-column sums over this context's walkers (olpe_moments_summary)."""
+        out = np.empty(self.moments_len)
+        c = None if centre is None else np.ascontiguousarray(centre, dtype=np.float64)
+        check(self._lib.olpe_moments_summary(self._ctx, _dptr(c), _dptr(out)))
         return out

@@ -6,15 +6,19 @@
 //   * all-gather of the final walker states      (ncclAllGather, rank-major)
 //   * all-gather of the chains (concatenation)   (ncclAllGather per walker range, so the
 //                                                 receive buffer is bounded by the range)
-//   * all-reduce of per-parameter moment sums    (ncclAllReduce, sum)
+//   * the posterior summary from the whole-run moments (olpe_moments.hip): two
+//     all-reduces (sum) -- the pooled mean, then the walkers' deviations about it
 // The reference's equivalent is one chain file per MPI rank behind the lockstep
 // barrier (apf_step2.py:338, :355-360).  RCCL gathers need equal counts on every rank:
-// each gather first all-reduces {W, -W, rows, -rows} (max) and returns OLPE_EINVAL on
-// every rank when the shards differ, instead of hanging or mixing rows.
+// each gather first all-reduces {W, -W, rows, -rows, range, -range, bad} (max) and
+// returns OLPE_EINVAL on every rank when the shards or the requested ranges differ or a
+// range is invalid on some rank, instead of hanging or mixing rows.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <string.h>
+
+#include <vector>
 
 #include "../../include/olpe.h"
 #include "olpe_internal.h"
@@ -22,34 +26,6 @@
 using olpe::set_err;
 
 namespace {
-
-// sums[k] / sumsq[k] over `rows` samples of a [rows][ps] array (one block per k)
-__global__ __launch_bounds__(256) void moments_kernel(const double *x, long long rows, int ps,
-                                                      double *out) {
-  __shared__ double s1[256], s2[256];
-  const int k = blockIdx.x;
-  double a = 0.0, b = 0.0;
-  for (long long r = threadIdx.x; r < rows; r += blockDim.x) {
-    const double v = x[r * ps + k];
-    a += v;
-    b += v * v;
-  }
-  s1[threadIdx.x] = a;
-  s2[threadIdx.x] = b;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      s1[threadIdx.x] += s1[threadIdx.x + o];
-      s2[threadIdx.x] += s2[threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    out[1 + k] = s1[0];
-    out[1 + ps + k] = s2[0];
-    if (k == 0) out[0] = (double)rows;
-  }
-}
 
 #define NCCLCHK(expr)                                                                   \
   do {                                                                                  \
@@ -99,15 +75,17 @@ int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   return OLPE_OK;
 }
 
-// every rank has the same W and (if rows >= 0) the same chain rows; the verdict is
-// the same on every rank, so a mismatch is an error everywhere and nothing hangs
-static int check_uniform(olpe_ctx *c, long long rows) {
-  long long h[4] = {c->W, -(long long)c->W, rows, -rows};
+// every rank has the same W, the same chain rows and the same gather range, and the
+// range is valid everywhere; the verdict is the same on every rank (one max
+// all-reduce), so a mismatch is an error everywhere and nothing hangs
+static int check_uniform(olpe_ctx *c, long long rows, long long w0 = 0, long long wn = 0,
+                         bool bad_range = false) {
+  long long h[9] = {c->W, -(long long)c->W, rows, -rows, w0, -w0, wn, -wn, bad_range ? 1 : 0};
   long long *d = nullptr;
   HIPCHK(hipMalloc(&d, sizeof(h)));
   hipError_t e = hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
   ncclResult_t r = ncclSuccess;
-  if (e == hipSuccess) r = ncclAllReduce(d, d, 4, ncclInt64, ncclMax, (ncclComm_t)c->comm, c->stream);
+  if (e == hipSuccess) r = ncclAllReduce(d, d, 9, ncclInt64, ncclMax, (ncclComm_t)c->comm, c->stream);
   if (e == hipSuccess && r == ncclSuccess)
     e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
@@ -118,7 +96,11 @@ static int check_uniform(olpe_ctx *c, long long rows) {
     return set_err(OLPE_EINVAL, "walkers per rank differ (%lld..%lld): RCCL gathers need equal "
                    "shards", -h[1], h[0]);
   if (h[2] != -h[3])
-    return set_err(OLPE_EINVAL, "chain rows per rank differ (%lld..%lld)", -h[3], h[2]);
+    return set_err(OLPE_EINVAL, "rows per rank differ (%lld..%lld)", -h[3], h[2]);
+  if (h[8])
+    return set_err(OLPE_EINVAL, "walker range outside [0, %d) on some rank", c->W);
+  if (h[4] != -h[5] || h[6] != -h[7])
+    return set_err(OLPE_EINVAL, "ranks asked for different walker ranges");
   return OLPE_OK;
 }
 
@@ -150,11 +132,16 @@ int olpe_comm_allgather_chain(olpe_ctx *c, long long w0, long long wn, double *o
   if (!c->comm) return set_err(OLPE_ESTATE, "call olpe_comm_init first");
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
+  // the range is validated locally and its verdict travels with the uniformity check,
+  // so a rank with a bad range cannot leave the others waiting in the gather
+  const bool bad = w0 < 0 || wn < 0 || w0 + wn > c->W;
   int rc;
-  if ((rc = check_uniform(c, c->chain_rows))) return rc;
+  if ((rc = check_uniform(c, c->chain_rows, w0, wn, bad))) {
+    if (bad)
+      return set_err(OLPE_EINVAL, "walker range [%lld, %lld) outside [0, %d)", w0, w0 + wn, c->W);
+    return rc;
+  }
   if (nrec_out) *nrec_out = c->chain_rows;
-  if (w0 < 0 || wn < 0 || w0 + wn > c->W)
-    return set_err(OLPE_EINVAL, "walker range [%lld, %lld) outside [0, %d)", w0, w0 + wn, c->W);
   const size_t row = (size_t)c->chain_rows * c->ps;     // doubles per walker
   const size_t per = (size_t)wn * row;                  // doubles per rank in this range
   if (per == 0) return OLPE_OK;
@@ -182,23 +169,44 @@ int olpe_comm_allreduce_moments(olpe_ctx *c, double *out) {
   if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
-  const int m = 1 + 2 * c->ps;
+  int rc;
+  if (c->comm && (rc = check_uniform(c, c->mom_n))) return rc;
+  const int ps = c->ps;
+  const size_t len = (size_t)OLPE_MOMENTS_LEN(ps, c->np);
   double *d = nullptr;
-  HIPCHK(hipMalloc(&d, m * sizeof(double)));
-  const bool chain = c->chain_rows > 0;
-  const double *src = chain ? c->d_chain : c->d_state;
-  const long long rows = chain ? (long long)c->W * c->chain_rows : (long long)c->W;
-  hipLaunchKernelGGL(moments_kernel, dim3(c->ps), dim3(256), 0, c->stream, src, rows, c->ps, d);
-  hipError_t e = hipGetLastError();
+  HIPCHK(hipMalloc(&d, (len + ps) * sizeof(double)));
+  double *dcen = d + len;
+  // round 1: every column's sums over all ranks; slot 1 sums to the walker total
+  // (slot 0 stays 0: n is the same on every rank, checked above)
+  double h01[2] = {0.0, (double)c->W};
+  std::vector<double> cen(ps);
+  hipError_t e = hipMemcpyAsync(d, h01, sizeof(h01), hipMemcpyHostToDevice, c->stream);
   ncclResult_t r = ncclSuccess;
-  if (e == hipSuccess && c->comm)
-    r = ncclAllReduce(d, d, m, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
-  if (e == hipSuccess && r == ncclSuccess)
-    e = hipMemcpyAsync(out, d, m * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  rc = e == hipSuccess ? olpe_moments_local(c, nullptr, d) : OLPE_OK;
+  if (e == hipSuccess && !rc && c->comm)
+    r = ncclAllReduce(d, d, len, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
+  if (e == hipSuccess && !rc && r == ncclSuccess)
+    e = hipMemcpyAsync(out, d, len * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && !rc && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  // round 2: the deviations of the walkers' means about the pooled mean
+  if (e == hipSuccess && !rc && r == ncclSuccess) {
+    for (int k = 0; k < ps; ++k) cen[k] = out[1] > 0 ? out[2 + k] / out[1] : 0.0;
+    e = hipMemcpyAsync(dcen, cen.data(), ps * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) rc = olpe_moments_local(c, dcen, d);
+    double *dev = d + 2 + 2 * ps;
+    if (e == hipSuccess && !rc && c->comm)
+      r = ncclAllReduce(dev, dev, ps, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
+    if (e == hipSuccess && !rc && r == ncclSuccess)
+      e = hipMemcpyAsync(out + 2 + 2 * ps, dev, ps * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream);
+    if (e == hipSuccess && !rc && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  }
+  (void)hipStreamSynchronize(c->stream);
   (void)hipFree(d);
+  if (rc) return rc;
   if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-  if (e != hipSuccess) return set_err(OLPE_EHIP, "moments: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return set_err(OLPE_EHIP, "moments all-reduce: %s", hipGetErrorString(e));
+  out[0] = (double)c->mom_n;
   return OLPE_OK;
 }
 

@@ -11,6 +11,12 @@
 // same bytes (std::to_chars gives the shortest round-trip digits, like repr) and
 // writes one file per walker from a pool of threads: at 10^5 walkers x 10^2 rows the
 // Python formatter takes minutes, this one the time of the disk writes.
+//
+// The reader is step 3's side of the same files (apf_step3.py:169-186: one
+// np.genfromtxt(..., delimiter=',') per walker file, collated into [rows, walkers]
+// arrays): it parses every file from a pool of threads straight into that layout.
+// std::from_chars rounds correctly, as Python's float() does, so the values are the
+// ones genfromtxt returns, bit for bit.
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -189,6 +195,156 @@ int olpe_csv_append_chains(const char *const *paths, const double *chains, int n
                            long long *sizes_out) {
   return write_files("olpe_csv_append_chains", paths, chains, nfiles, rows_per_file, nrows,
                      ncols, false, threads, "ab", sizes_out);
+}
+
+}  // extern "C"
+
+// --- reader (apf_step3.py:169-186) -------------------------------------------------
+namespace {
+
+bool read_all(const char *path, std::vector<char> &buf) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  bool ok = fseek(f, 0, SEEK_END) == 0;
+  const long size = ok ? ftell(f) : -1;
+  ok = ok && size >= 0 && fseek(f, 0, SEEK_SET) == 0;
+  if (ok) {
+    buf.resize((size_t)size);
+    ok = fread(buf.data(), 1, (size_t)size, f) == (size_t)size;
+  }
+  fclose(f);
+  return ok;
+}
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+
+// one field as np.genfromtxt's float converter reads it: surrounding blanks stripped, an
+// empty field is missing (NaN), 'nan' / 'inf' / '-inf' and a leading '+' accepted
+bool parse_field(const char *a, const char *b, double &v) {
+  while (a < b && is_space(*a)) ++a;
+  while (b > a && is_space(b[-1])) --b;
+  if (a == b) {
+    v = std::nan("");
+    return true;
+  }
+  if (*a == '+') ++a;
+  const std::from_chars_result r = std::from_chars(a, b, v);
+  return r.ec == std::errc() && r.ptr == b;
+}
+
+bool blank(const char *a, const char *b) {
+  while (a < b && is_space(*a)) ++a;
+  return a == b;
+}
+
+// the lines of buf (without the terminator); blank lines are skipped, as genfromtxt does
+template <class F> bool for_lines(const std::vector<char> &buf, F &&fn) {
+  const char *p = buf.data(), *end = p + buf.size();
+  while (p < end) {
+    const char *eol = (const char *)memchr(p, '\n', (size_t)(end - p));
+    if (!eol) eol = end;
+    if (!blank(p, eol) && !fn(p, eol)) return false;
+    p = eol + 1;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int olpe_csv_shape(const char *path, long long *rows, int *cols) {
+  if (!path || !rows || !cols) return olpe::set_err(OLPE_EINVAL, "olpe_csv_shape: NULL argument");
+  std::vector<char> buf;
+  if (!read_all(path, buf)) return olpe::set_err(OLPE_EIO, "olpe_csv_shape: cannot read %s", path);
+  long long n = 0;
+  int c = 0;
+  for_lines(buf, [&](const char *a, const char *b) {
+    if (n++ == 0) {
+      c = 1;
+      for (const char *q = a; q < b; ++q) c += *q == ',';
+    }
+    return true;
+  });
+  *rows = n;
+  *cols = c;
+  return OLPE_OK;
+}
+
+int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, int ncols,
+                         long long skip, double *out, int threads) {
+  if (!paths || nfiles < 0 || nrows < 0 || ncols <= 0 || skip < 0 || skip > nrows ||
+      (!out && nfiles > 0 && nrows > skip))
+    return olpe::set_err(OLPE_EINVAL, "olpe_csv_read_chains: bad arguments");
+  for (int i = 0; i < nfiles; ++i)
+    if (!paths[i]) return olpe::set_err(OLPE_EINVAL, "olpe_csv_read_chains: path %d is NULL", i);
+  unsigned nt = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
+  if (nt == 0) nt = 1;
+  if (nt > 64) nt = 64;
+  if (nt > (unsigned)nfiles) nt = (unsigned)(nfiles > 0 ? nfiles : 1);
+  // per thread: the first failing file and what went wrong
+  std::vector<int> failed(nt, -1);
+  std::vector<std::string> why(nt);
+  auto work = [&](unsigned t) {
+    std::vector<char> buf;
+    char msg[160];
+    for (int i = (int)t; i < nfiles; i += (int)nt) {
+      if (!read_all(paths[i], buf)) {
+        failed[t] = i;
+        why[t] = "cannot read";
+        return;
+      }
+      long long row = 0;
+      const bool ok = for_lines(buf, [&](const char *a, const char *b) {
+        if (row >= nrows) {
+          snprintf(msg, sizeof(msg), "more than %lld rows (walker 0's length)", nrows);
+          return false;
+        }
+        double *dst = out ? out + ((size_t)(row - skip) * (size_t)nfiles + (size_t)i) * (size_t)ncols
+                          : nullptr;
+        int col = 0;
+        const char *f = a;
+        for (;;) {
+          const char *comma = (const char *)memchr(f, ',', (size_t)(b - f));
+          const char *fe = comma ? comma : b;
+          double v;
+          if (col >= ncols) {
+            snprintf(msg, sizeof(msg), "row %lld has more than %d fields", row, ncols);
+            return false;
+          }
+          if (!parse_field(f, fe, v)) {
+            snprintf(msg, sizeof(msg), "row %lld field %d is not a number", row, col);
+            return false;
+          }
+          if (row >= skip) dst[col] = v;
+          ++col;
+          if (!comma) break;
+          f = comma + 1;
+        }
+        if (col != ncols) {
+          snprintf(msg, sizeof(msg), "row %lld has %d fields, not %d", row, col, ncols);
+          return false;
+        }
+        ++row;
+        return true;
+      });
+      if (ok && row != nrows) snprintf(msg, sizeof(msg), "%lld rows, not %lld", row, nrows);
+      if (!ok || row != nrows) {
+        failed[t] = i;
+        why[t] = msg;
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto &th : pool) th.join();
+  for (unsigned t = 0; t < nt; ++t)
+    if (failed[t] >= 0)
+      return olpe::set_err(failed[t] >= 0 && why[t] == "cannot read" ? OLPE_EIO : OLPE_EINVAL,
+                           "olpe_csv_read_chains: %s: %s", paths[failed[t]], why[t].c_str());
+  return OLPE_OK;
 }
 
 }  // extern "C"

@@ -60,6 +60,15 @@ struct olpe_ctx {
   int ring_wpb = 12;        // 128x128 FAST: the lockstep LDS-ring sampler's waves per
                             // workgroup, 0 = the L2-resident sampler (OLPE_RING)
   int stagger = 0;          // wave start offsets (OLPE_STAGGER)
+  // whole-run moments of the recorded rows (olpe_moments.hip): running mean / M2 per
+  // walker and column, [ps][W]; mom_n rows folded per walker; mom_folded = the launch
+  // whose rows were folded last (a launch is folded at most once)
+  double *d_mmean = nullptr, *d_mm2 = nullptr;
+  size_t mom_cap = 0;
+  long long mom_n = 0;
+  long long mom_folded = 0;
+  double *d_mpart = nullptr;    // partial sums of olpe_moments_local
+  size_t mpart_cap = 0;
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;
@@ -71,3 +80,5 @@ namespace olpe {
 int set_err(int code, const char *fmt, ...);
 }
 void olpe_comm_release(olpe_ctx *c);
+// per-column sums over this context's walkers into d_out[2 ..] (olpe_moments.hip)
+int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out);

@@ -14,15 +14,19 @@ Output is streamed.  The reference rewrites every file each 10 iterations
 launch (a *chunk*, a multiple of 10 iterations) appends its rows to the per-walker
 files and rewrites the acceptance files, so the files always hold what the
 reference's files hold at that count, host memory is bounded by one chunk, and a
-checkpoint (walker state, counters, RNG streams, file sizes) after each chunk makes a
-killed run resumable (``--resume``) with the same chains as an uninterrupted one.
+checkpoint (walker state, counters, RNG streams, moments, file sizes) at most once a
+minute (``--checkpoint-secs``) makes a killed run resumable (``--resume``) with the same
+chains as an uninterrupted one.  Every launch's rows are also folded into per-walker
+moments on the device, and the run ends by writing ``posterior_summary.json``: step 3's
+means, sigmas, Gelman-Rubin PSRF / RC and acceptance (apf_step3.py:258-278,
+apf_step2.py:362-365) without reading a chain back.
 
 Launched like the reference (``mpiexec -n W python apf_step2.py <image>``), rank 0 runs
 all W walkers and the other ranks exit (``MPI_ENV``).  Added flags: ``--walkers`` (the
 reference's MPI size), ``--seed``, ``--iters`` (fixed
 length instead of accept_min), ``--record-stride``, ``--gpus``, ``--exact``,
-``--fixed-bkgd``, ``--chunk``, ``--mem-budget``, ``--checkpoint-every``, ``--resume``,
-``--no-csv``, ``--npy``.
+``--fixed-bkgd``, ``--chunk``, ``--mem-budget``, ``--checkpoint-secs``,
+``--checkpoint-every``, ``--resume``, ``--no-csv``, ``--npy``.
 """
 from __future__ import annotations
 
@@ -32,10 +36,11 @@ import json
 import os
 import sys
 import threading
+import time
 
 import numpy as np
 
-from . import _lib, fitsio, pipeline
+from . import _lib, fitsio, pipeline, step3
 from .core import Sampler
 
 MAX_CHUNK = 20000          # iterations per launch when memory allows
@@ -98,8 +103,12 @@ def parse(argv, nsrc, variant="2"):
     ap.add_argument("--mem-budget", type=float, default=1.0,
                     help="GiB of chain rows per launch (host copy; the device buffer is "
                          "also kept under a quarter of free device memory)")
-    ap.add_argument("--checkpoint-every", type=int, default=1,
-                    help="write a resumable checkpoint every N launches (0 = never)")
+    ap.add_argument("--checkpoint-secs", type=float, default=60.0,
+                    help="write a resumable checkpoint after a launch when this many seconds "
+                         "have passed since the last one (0 = no time-based checkpoints); a "
+                         "checkpoint holds the MT keys, 2.5 KB per walker")
+    ap.add_argument("--checkpoint-every", type=int, default=0,
+                    help="also write one every N launches (0 = only by time)")
     ap.add_argument("--resume", action="store_true",
                     help="continue the run recorded in the output directory's checkpoint")
     ap.add_argument("--no-csv", action="store_true")
@@ -134,6 +143,7 @@ class Shard:
         self.last = None                 # the last launch's chain [W, nrec, PS]
 
     def snapshot(self):
+        # (the moments need no snapshot: a launch is folded in only when it is kept)
         return self.s.get_state(), self.s.rng_state(), self.s.count
 
     def restore(self, snap):
@@ -215,9 +225,16 @@ class Output:
                                            np.zeros((sh.W, 0, sh.s.ps)), 0, 0)
 
     def truncate(self, sizes, npy_rows):
-        """Back to a checkpoint: rows appended after it are dropped (they are re-run)."""
+        """Back to a checkpoint: rows appended after it are dropped (they are re-run).
+        A file shorter than the checkpoint recorded is not this run's: refused (a
+        truncate would pad it with NUL bytes)."""
         for g, sh in enumerate(self.shards):
             if self.csv:
+                for p, n in zip(self._paths(g, 0), sizes[sh.w0:sh.w0 + sh.W]):
+                    have = os.path.getsize(p) if os.path.exists(p) else -1
+                    if have < int(n):
+                        raise ValueError(f"--resume: {p} holds {have} bytes, fewer than the "
+                                         f"{int(n)} the checkpoint recorded: not this run's file")
                 for p, n in zip(self._paths(g, 0), sizes[sh.w0:sh.w0 + sh.W]):
                     with open(p, "r+b") as f:
                         f.truncate(int(n))
@@ -235,6 +252,8 @@ class Output:
         def body(g):
             sh = self.shards[g]
             rows = sh.last.shape[1]
+            if rows:
+                sh.s.moments_accumulate()        # async, on the device
             _, tries, acc = sh.s.get_state()
             if self.csv:
                 if rows:
@@ -264,14 +283,18 @@ def checkpoint_path(outdir, variant):
 
 
 def save_checkpoint(path, shards, out, count, config):
-    st, tr, ac, mt, ga = [], [], [], [], []
+    st, tr, ac, mt, ga, mm, mq = [], [], [], [], [], [], []
+    nmom = 0
     for sh in shards:
         s, t, a = sh.s.get_state()
         m, g = sh.s.rng_state()
+        nmom, mmean, mm2 = sh.s.moments()
         st.append(s), tr.append(t), ac.append(a), mt.append(m), ga.append(g)
+        mm.append(mmean), mq.append(mm2)
     tmp = path + ".tmp.npz"
     np.savez(tmp, state=np.concatenate(st), tries=np.concatenate(tr),
              accepts=np.concatenate(ac), mt=np.concatenate(mt), gauss=np.concatenate(ga),
+             mom_n=np.int64(nmom), mom_mean=np.concatenate(mm), mom_m2=np.concatenate(mq),
              count=np.int64(count), csv_sizes=out.all_sizes(), npy_rows=np.int64(out.npy_rows),
              config=np.array(json.dumps(config, sort_keys=True)))
     os.replace(tmp, path)
@@ -280,6 +303,19 @@ def save_checkpoint(path, shards, out, count, config):
 def load_checkpoint(path):
     with np.load(path, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+def run_id_path(outdir, variant):
+    return outdir + ("step2_run_id" if variant == "2" else "step2a_run_id")
+
+
+def posterior_summary(shards, nsrc):
+    """step3.summary_from_moments over every shard's walkers (two passes: the pooled
+    mean, then the walkers' deviations about it)."""
+    parts = [sh.s.moments_summary() for sh in shards]
+    centre = step3.pooled_mean(parts)
+    dev = [sh.s.moments_summary(centre) for sh in shards]
+    return step3.summary_from_moments(step3.combine_moments(parts, dev), nsrc)
 
 
 def main(argv=None, nsrc=2, variant="2"):
@@ -307,7 +343,15 @@ def main(argv=None, nsrc=2, variant="2"):
               "fixed_bkgd": args.fixed_bkgd, "csv": not args.no_csv, "npy": args.npy}
     if resume is not None:
         old = json.loads(str(resume["config"]))
-        base, p0 = old.pop("seed"), np.array(old.pop("p0"))
+        base, p0, run_id = old.pop("seed"), np.array(old.pop("p0")), old.pop("run_id", None)
+        try:
+            with open(run_id_path(outdir, variant)) as f:
+                on_disk = f.read().strip()
+        except OSError:
+            on_disk = None
+        if run_id is None or on_disk != run_id:
+            raise ValueError(f"--resume: {ckpt} belongs to run {run_id}, the files in {outdir} "
+                             f"to run {on_disk}")
         if old != config:
             diff = {k: (old.get(k), config.get(k)) for k in set(old) | set(config)
                     if old.get(k) != config.get(k)}
@@ -322,7 +366,8 @@ def main(argv=None, nsrc=2, variant="2"):
             guess = pipeline.read_guess(directory + frame + "_initialguess")
             p0 = pipeline.initial_parameters(image, guess, nsrc)
         base = args.seed if args.seed is not None else int.from_bytes(os.urandom(4), "little")
-    config.update(seed=base, p0=[float(v) for v in p0])
+        run_id = os.urandom(8).hex()
+    config.update(seed=base, p0=[float(v) for v in p0], run_id=run_id)
     W = args.walkers
     seeds = (base + np.arange(W, dtype=np.int64)) & 0xFFFFFFFF
     say(f"walkers {W}, seeds {base}..{base + W - 1} (np.random.seed semantics)")
@@ -341,20 +386,38 @@ def main(argv=None, nsrc=2, variant="2"):
             sl = slice(sh.w0, sh.w0 + sh.W)
             sh.restore(((resume["state"][sl], resume["tries"][sl], resume["accepts"][sl]),
                         (resume["mt"][sl], resume["gauss"][sl]), count))
+        if "mom_n" in resume:
+            for sh in shards:
+                sl = slice(sh.w0, sh.w0 + sh.W)
+                sh.s.set_moments(int(resume["mom_n"]), resume["mom_mean"][sl],
+                                 resume["mom_m2"][sl])
         out.truncate(resume["csv_sizes"], int(resume["npy_rows"]))
     else:
+        # a fresh run: a checkpoint left by an earlier run in this directory must not be
+        # resumable against the files rewritten now
+        if os.path.exists(ckpt):
+            os.remove(ckpt)
+        with open(run_id_path(outdir, variant), "w") as f:
+            f.write(run_id + "\n")
         out.start()
 
     burn, stride = args.burn_in, args.record_stride
     chunk = chunk_size(shards, stride, args.chunk, args.mem_budget)
     launches = 0
+    last_ckpt = time.monotonic()
 
     def commit():
-        nonlocal launches
+        # checkpoints are spaced by time (and optionally by launches), not written per
+        # launch: one holds every walker's MT key (190 MB at 65,536 walkers)
+        nonlocal launches, last_ckpt
         out.commit(acceptance=count >= burn)
         launches += 1
-        if args.checkpoint_every and launches % args.checkpoint_every == 0:
+        now = time.monotonic()
+        due = (args.checkpoint_every and launches % args.checkpoint_every == 0) or \
+              (args.checkpoint_secs > 0 and now - last_ckpt >= args.checkpoint_secs)
+        if due:
             save_checkpoint(ckpt, shards, out, count, config)
+            last_ckpt = time.monotonic()
 
     def run(n, accept_min=0, record=True):
         _parallel(shards, lambda sh: sh.run(n, burn, stride if record else 0, accept_min))
@@ -396,6 +459,13 @@ def main(argv=None, nsrc=2, variant="2"):
                 commit()
             say("Loop count:", count)
             break
+    if variant == "2":
+        summ = posterior_summary(shards, nsrc)
+        with open(outdir + "posterior_summary.json", "w") as f:
+            json.dump(summ, f, indent=1)
+        if summ["_rows_per_walker"] > 1:
+            say("Posterior (device moments):", {k: round(summ[k]["mean"], 6)
+                                                for k in list(summ)[:4]})
     if os.path.exists(ckpt):
         os.remove(ckpt)                  # the run is complete: nothing to resume
     for sh in shards:

@@ -7,6 +7,7 @@ stages.  This module is that read + statistics front end, usable on the build's 
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import numpy as np
@@ -18,22 +19,46 @@ NAMES_3 = ["xca", "yca", "xcb", "ycb", "xcc", "ycc", "dx", "dy", "ampa", "ampb",
            "chisquare"]
 
 
-def load_chains(input_directory: str, ncor: int, additional_burnin: int = 1):
+def load_chains(input_directory: str, ncor: int, additional_burnin: int = 1,
+                source: str = "csv", threads: int = 0):
     """apf_step3.py:169-205: returns an array [length - additional_burnin, ncor, PS].
 
     The chain length is taken from walker 0 and every walker file must have it (the
-    reference assigns columns into [length, ncor] arrays, :174-186)."""
-    first = np.genfromtxt(os.path.join(input_directory, "0_finalarray_mpi.csv"), delimiter=",")
-    first = np.atleast_2d(first)
-    length, ps = first.shape
-    out = np.zeros((length, ncor, ps))
-    for i in range(ncor):
-        a = np.atleast_2d(np.genfromtxt(os.path.join(input_directory, f"{i}_finalarray_mpi.csv"),
-                                        delimiter=","))
-        if a.shape != (length, ps):
-            raise ValueError(f"walker {i}: chain shape {a.shape} != walker 0's {(length, ps)}")
-        out[:, i, :] = a
-    return out[additional_burnin:length]
+    reference assigns columns into [length, ncor] arrays, :174-186).  ``source="csv"``
+    parses the ``{i}_finalarray_mpi.csv`` files natively from a pool of threads
+    (olpe_csv_read_chains: the values np.genfromtxt returns, bit for bit);
+    ``source="npy"`` reads the ``{i}_chain.npy`` sidecars step 2 writes with ``--npy``
+    (the same rows without the NaN seed row, which counts as one burn-in row)."""
+    from . import _lib
+    if source == "npy":
+        paths = [os.path.join(input_directory, f"{i}_chain.npy") for i in range(ncor)]
+        first = np.load(paths[0], mmap_mode="r")
+        length, ps = first.shape[0] + 1, first.shape[1]
+        out = np.empty((max(0, length - additional_burnin), ncor, ps))
+        lo = max(0, additional_burnin - 1)
+        for i, p in enumerate(paths):
+            a = np.load(p, mmap_mode="r")
+            if a.shape != first.shape:
+                raise ValueError(f"walker {i}: chain shape {a.shape} != walker 0's {first.shape}")
+            out[:, i, :] = a[lo:]
+        return out
+    if source != "csv":
+        raise ValueError("source must be 'csv' or 'npy'")
+    lib = _lib.load()
+    paths = [os.fsencode(os.path.join(input_directory, f"{i}_finalarray_mpi.csv"))
+             for i in range(ncor)]
+    rows, cols = C.c_longlong(0), C.c_int(0)
+    _lib.check(lib.olpe_csv_shape(paths[0], C.byref(rows), C.byref(cols)))
+    length, ps = rows.value, cols.value
+    skip = min(max(0, int(additional_burnin)), length)
+    out = np.empty((length - skip, ncor, ps))
+    arr = (C.c_char_p * ncor)(*paths)
+    rc = lib.olpe_csv_read_chains(arr, ncor, length, ps, skip,
+                                  out.ctypes.data_as(C.POINTER(C.c_double)), int(threads))
+    if rc == _lib.EINVAL:
+        raise ValueError(lib.olpe_last_error().decode(errors="replace"))
+    _lib.check(rc)
+    return out
 
 
 def gelman_rubin(p, d: int = 16):
@@ -73,3 +98,66 @@ def summary(chains, nsrc: int = 2):
         out[name] = {"mean": float(np.mean(x)), "median": float(np.median(x)),
                      "std": float(np.std(x)), "gr_psrf": float(psrf), "gr_rc": float(rc)}
     return out
+
+
+def summary_from_moments(m, nsrc: int = 2, d: int = 16):
+    """The statistics of ``summary`` (minus the median, which no moment gives) from the
+    device-accumulated whole-run moments -- ``Sampler.allreduce_moments()``, the
+    olpe_moments_summary layout with the centre at the pooled mean -- without reading a
+    chain.  Over N rows per walker (all recorded rows: step 3's default
+    additional_burnin = 1) and M walkers, as apf_step3.py:258-278 computes them:
+
+    * mean = sum_w mean_w / M (= np.mean over all rows: every walker has N rows);
+    * std = sqrt((sum_w M2_w + N sum_w (mean_w - mean)^2) / (N M)) (np.std over all rows);
+    * w = (1/M) sum_w M2_w / N, b = N/(M-1) sum_w (mean_w - mean)^2, PSRF =
+      ((N-1)/N w + (M+1)/(M N) b) / w, RC = sqrt(((d+3)//(d+1)) PSRF) (Python 2's
+      integer division, see gelman_rubin);
+    * acceptance = whole-run accepts / tries per parameter (apf_step2.py:362-365)."""
+    names = NAMES_2 if nsrc == 2 else NAMES_3
+    m = np.asarray(m, dtype=np.float64)
+    ps = len(names)
+    np_ = ps - 1
+    if m.shape != (2 + 3 * ps + 2 * np_,):
+        raise ValueError(f"moments vector of length {m.size}, expected {2 + 3 * ps + 2 * np_}")
+    N, M = np.float64(m[0]), np.float64(m[1])      # NumPy floats: M = 1 gives NaN, not a raise
+    sums, m2, dev = m[2:2 + ps], m[2 + ps:2 + 2 * ps], m[2 + 2 * ps:2 + 3 * ps]
+    tries, acc = m[2 + 3 * ps:2 + 3 * ps + np_], m[2 + 3 * ps + np_:]
+    factor = (d + 3) // (d + 1) if isinstance(d, (int, np.integer)) else (d + 3) / (d + 1)
+    out = {}
+    with np.errstate(all="ignore"):
+        for k, name in enumerate(names):
+            mean = sums[k] / M
+            std = np.sqrt((m2[k] + N * dev[k]) / (N * M))
+            ent = {"mean": float(mean), "std": float(std)}
+            if k < np_:
+                w = (1. / M) * (m2[k] / N)
+                b = (N / (M - 1)) * dev[k]
+                psrf = (((N - 1) / N) * w + ((M + 1) / (M * N)) * b) / w
+                ent.update(gr_psrf=float(psrf), gr_rc=float(np.sqrt(factor * psrf)),
+                           acceptance=float(acc[k] / tries[k]), tries=float(tries[k]),
+                           accepts=float(acc[k]))
+            out[name] = ent
+    out["_rows_per_walker"] = int(N)
+    out["_walkers"] = int(M)
+    return out
+
+
+def combine_moments(parts, centre_parts):
+    """One summary vector from several contexts of one process (step 2's ``--gpus``
+    shards): ``parts`` = each context's ``moments_summary()`` (no centre),
+    ``centre_parts`` = each context's ``moments_summary(centre)`` about the pooled mean
+    of ``parts`` (``pooled_mean(parts)``)."""
+    parts = np.asarray(parts)
+    out = parts.sum(axis=0)
+    out[0] = parts[0][0]
+    if not np.all(parts[:, 0] == parts[0][0]):
+        raise ValueError("contexts folded different numbers of rows")
+    ps = out.size // 5                 # OLPE_MOMENTS_LEN = 2 + 3 PS + 2 (PS - 1)
+    out[2 + 2 * ps:2 + 3 * ps] = np.asarray(centre_parts)[:, 2 + 2 * ps:2 + 3 * ps].sum(axis=0)
+    return out
+
+
+def pooled_mean(parts):
+    parts = np.asarray(parts)
+    ps = parts.shape[1] // 5
+    return parts[:, 2:2 + ps].sum(axis=0) / parts[:, 1].sum()

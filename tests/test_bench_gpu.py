@@ -1,0 +1,44 @@
+"""bench.py on the GPU: the N > 1 end-of-run exchange code run with a one-rank RCCL
+communicator (--exchange), which is what can be checked before a multi-GPU lease: the
+state all-gather, the moments all-reduce and the range-wise chain all-gather, with every
+gathered range compared against the rank's own chain rows (--verify-exchange)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=300):
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=REPO, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_bench_exchange_one_rank():
+    W = 2048
+    d = _bench("--exchange", "--verify-exchange", "--walkers", str(W), "--steps", "2",
+               "--warmup", "1", "--gather-mib", "1", "--no-cpu-baseline", "--no-alt")
+    assert "comm_error" not in d, d.get("comm_error")
+    assert d["n_gpus"] == 1 and d["exchange_verified"] is True
+    per_walker = 10 * 17 * 8                         # 100 iterations at stride 10, PS = 17
+    assert d["chain_gather_bytes"] == W * per_walker
+    assert d["chain_gather_range_walkers"] == 2 ** 20 // per_walker
+    assert d["chain_gather_ranges"] == -(-W // (2 ** 20 // per_walker))
+    assert d["chain_gather_ms"] > 0 and d["chain_gather_gbs"] is None     # one rank
+    assert d["allgather_ms"] > 0 and d["moments_allreduce_ms"] > 0
+    p = d["posterior"]
+    assert p["walkers"] == W and p["rows_per_walker"] == 3 * 10        # warm-up + 2 steps
+    assert 0 < p["acceptance"] < 1 and abs(p["means"]["xcs"] - 31.7) < 0.6
+
+
+def test_bench_default_line_has_posterior_and_profile():
+    d = _bench("--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-alt")
+    assert d["posterior"]["walkers"] == 65536 and d["posterior"]["rows_per_walker"] == 30
+    r = d["roofline"]
+    assert r["frac_source"] == "counters" and 0 < r["frac"] <= 1

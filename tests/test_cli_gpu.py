@@ -183,7 +183,8 @@ def test_cli_resume_after_interrupt(tmp_path, monkeypatch, mode):
     streams, and every file ends byte-equal to an uninterrupted run's."""
     path = synth.write_case(str(tmp_path / "ref"), 32, 2)
     path2 = synth.write_case(str(tmp_path / "cut"), 32, 2)
-    run = ["--walkers", "3", "--seed", "21", "--burn-in", "15", "--chunk", "40", "--npy", "-q"]
+    run = ["--walkers", "3", "--seed", "21", "--burn-in", "15", "--chunk", "40", "--npy", "-q",
+           "--checkpoint-every", "1"]
     run += ["--iters", "205"] if mode == "iters" else ["--accept-min", "25"]
     ref = step2.main([path, *run])
     calls = {"n": 0}
@@ -246,3 +247,95 @@ def test_cli_host_memory_bounded_by_launch(tmp_path):
             assert np.all(np.isfinite(c[-iters // 10:]))
     grow = rss[8000] - rss[1000]
     assert grow < 40e6, (rss, grow)
+
+
+def test_cli_posterior_summary_from_device_moments(tmp_path):
+    """SURVEY.md §8(f) row 1 at configs[1]'s size: a 4,096-walker CLI run folds every
+    launch's rows into device moments and writes posterior_summary.json; its means,
+    sigmas and Gelman-Rubin PSRF / RC equal step3.summary over the chain files read back
+    through the step-3 contract (apf_step3.py:169-186, :258-278) at rtol 1e-12, and its
+    tries / accepts totals equal the walkers' acceptance counters."""
+    import json
+    W, iters, burn = 4096, 300, 100
+    path = synth.write_case(str(tmp_path), 64, 2)
+    out = step2.main([path, "--walkers", str(W), "--seed", "3", "--iters", str(iters),
+                      "--burn-in", str(burn), "--chunk", "70", "-q"])
+    with open(out + "posterior_summary.json") as f:
+        summ = json.load(f)
+    c = step3.load_chains(out, W)
+    assert c.shape == (iters - burn + 1, W, 17)
+    assert summ["_rows_per_walker"] == c.shape[0] and summ["_walkers"] == W
+    ref = step3.summary(c)
+    for name, r in ref.items():
+        for key in ("mean", "std", "gr_psrf", "gr_rc"):
+            np.testing.assert_allclose(summ[name][key], r[key], rtol=1e-12, err_msg=(name, key))
+    assert sum(summ[n]["tries"] for n in ref) == W * iters
+    rates = [np.array(open(out + f"{w}_acceptance_rate.csv").read().strip("[]").split(),
+                      dtype=float) for w in (0, 1)]
+    assert all(np.all((r >= 0) & (r <= 1)) for r in rates)
+
+
+def test_cli_checkpoints_spaced_by_time(tmp_path, monkeypatch):
+    """Checkpoints (each holds every walker's MT key) are written by time, not per
+    launch: 40 launches of a short run write none by default, one every 8 launches with
+    --checkpoint-every 8; the run still completes and removes its checkpoint."""
+    calls = []
+    orig = step2.save_checkpoint
+
+    def counting(*a, **k):
+        calls.append(1)
+        orig(*a, **k)
+    monkeypatch.setattr(step2, "save_checkpoint", counting)
+    for extra, want in (([], 0), (["--checkpoint-every", "8"], 5)):
+        calls.clear()
+        path = synth.write_case(str(tmp_path / f"r{want}"), 32, 2)
+        out = step2.main([path, "--walkers", "64", "--seed", "2", "--iters", "400", "--burn-in",
+                          "0", "--chunk", "10", "-q", *extra])
+        assert len(calls) == want
+        assert not os.path.exists(out + "step2_checkpoint.npz")
+
+
+def test_cli_resume_refuses_another_runs_files(tmp_path, monkeypatch):
+    """A fresh run removes a checkpoint an earlier run left in its directory, so a later
+    --resume cannot mix two runs; a checkpoint whose run id differs from
+    the files', or whose recorded file sizes exceed the files', is refused."""
+    path = synth.write_case(str(tmp_path), 32, 2)
+    run = ["--walkers", "2", "--seed", "5", "--iters", "200", "--burn-in", "0", "--chunk", "20",
+           "-q", "--checkpoint-every", "1"]
+    orig = step2.save_checkpoint
+    calls = {"n": 0}
+
+    def dying(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise KeyboardInterrupt("killed")
+        orig(*a, **k)
+    monkeypatch.setattr(step2, "save_checkpoint", dying)
+    with pytest.raises(KeyboardInterrupt):
+        step2.main([path, *run])                           # leaves a checkpoint
+    outdir = pipeline.image_paths(path)[2]
+    ck = outdir + "step2_checkpoint.npz"
+    assert os.path.exists(ck)
+    saved = open(ck, "rb").read()
+    calls["n"] = 2
+    with pytest.raises(KeyboardInterrupt):
+        step2.main([path, *run])                           # fresh run, killed early
+    assert not os.path.exists(ck)                          # the stale checkpoint is gone
+    with pytest.raises(FileNotFoundError):
+        step2.main([path, *run, "--resume"])
+    with open(ck, "wb") as f:                              # an old run's checkpoint back
+        f.write(saved)
+    with pytest.raises(ValueError, match="belongs to run"):
+        step2.main([path, *run, "--resume"])
+    monkeypatch.setattr(step2, "save_checkpoint", orig)
+    # same run id, but files shorter than the checkpoint recorded
+    with open(ck, "wb") as f:
+        f.write(saved)
+    z = dict(np.load(ck))
+    with open(outdir + "step2_run_id", "w") as f:
+        import json
+        f.write(json.loads(str(z["config"]))["run_id"] + "\n")
+    with open(outdir + "0_finalarray_mpi.csv", "r+b") as f:
+        f.truncate(10)
+    with pytest.raises(ValueError, match="fewer than"):
+        step2.main([path, *run, "--resume"])

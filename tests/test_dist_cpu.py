@@ -86,8 +86,8 @@ def test_shard_and_seed_helpers():
 
 def test_bench_comm_watchdog_reports_and_exits():
     """bench.py's watchdog of the end-of-run RCCL exchange: rank 0 prints its JSON line
-    with the timeout as comm_error and the process leaves with status 0 (the driver's
-    N > 1 line survives a hung collective)."""
+    with the timeout as comm_error (the measurement survives a hung collective) and the
+    process leaves with status 3, so the launcher sees the failure."""
     import json
     import subprocess
     import sys
@@ -98,6 +98,6 @@ def test_bench_comm_watchdog_reports_and_exits():
             "time.sleep(30)\n")
     r = subprocess.run([sys.executable, "-c", code], cwd=repo, capture_output=True,
                        text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
+    assert r.returncode == 3, r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["value"] == 1.0 and out["comm_error"].startswith("TimeoutError")

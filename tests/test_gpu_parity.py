@@ -277,7 +277,7 @@ def test_errors_are_reported(golden, lib_loaded):
 
 def test_rccl_single_rank_collectives(golden, lib_loaded):
     """RCCL communicator with one rank on the box's GPU: the all-gather returns the
-    walker states and the all-reduced moments equal NumPy's over the last chain."""
+    walker states and the all-reduced moment sums equal NumPy's over the chain."""
     from olpefit_amd.core import Sampler
     g = golden("c32")
     s = make_sampler(g)
@@ -287,11 +287,15 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     s.comm_init(Sampler.comm_unique_id(), 1, 0)
     st, _, _ = s.get_state()
     np.testing.assert_array_equal(s.allgather_state(), st)
-    m = s.allreduce_moments()
-    flat = chain.reshape(-1, s.ps)
-    assert m[0] == flat.shape[0]
-    np.testing.assert_allclose(m[1:1 + s.ps], flat.sum(axis=0), rtol=1e-12)
-    np.testing.assert_allclose(m[1 + s.ps:], (flat ** 2).sum(axis=0), rtol=1e-12)
+    s.moments_accumulate()
+    local = s.allreduce_moments()                        # one rank: this context alone
+    ps = s.ps
+    mean = chain.mean(axis=1)                            # [W, PS]
+    assert local[0] == chain.shape[1] and local[1] == 8
+    np.testing.assert_allclose(local[2:2 + ps], mean.sum(axis=0), rtol=1e-12)
+    np.testing.assert_allclose(local[2 + 2 * ps:2 + 3 * ps],
+                               ((mean - mean.mean(axis=0)) ** 2).sum(axis=0), rtol=1e-9,
+                               atol=1e-300)
     # chain concatenation, whole and range by range (bounded receive buffer)
     np.testing.assert_array_equal(s.allgather_chain()[0], chain)
     parts = [s.allgather_chain(w0, 3)[0] for w0 in (0, 3)] + [s.allgather_chain(6, 2)[0]]
@@ -299,6 +303,8 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     assert s.allgather_chain(2, 4, out=False) is None
     with pytest.raises(Exception):
         s.allgather_chain(6, 3)                          # past the last walker
+    # the moments all-reduce over the communicator equals the local two-pass summary
+    np.testing.assert_array_equal(s.allreduce_moments(), local)
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
@@ -811,3 +817,63 @@ def test_degenerate_runs(golden, lib_loaded, mode):
             ref, _ = ora.Walker(dm, err, g["p_init"], seeds[w]).run(120, burn_in=80,
                                                                      record_stride=3)
             np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+
+
+def test_moments_fold_matches_numpy(golden, lib_loaded):
+    """olpe_moments_accumulate over several launches (odd row counts, a launch with no
+    rows, 300 walkers: two summary blocks) keeps every walker's running mean and M2 of
+    all its recorded rows: equal to NumPy's two-pass values over the concatenated
+    chain (mean rel 1e-13, M2 rel 1e-10); the summary sums, the pooled-centre
+    deviations and the tries / accepts totals follow; a launch cannot be folded twice;
+    get / set round-trips (checkpoints)."""
+    from olpefit_amd import step3
+    from olpefit_amd.core import OlpeError
+    g = golden("c32")
+    W = 300
+    s = make_sampler(g, "fast")
+    s.seed(np.arange(70, 70 + W))
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    parts = []
+    for n in (57, 3, 1, 140):
+        c = s.run(n, burn_in=20, record_stride=3)
+        s.moments_accumulate()
+        if c is not None:
+            parts.append(c)
+    with pytest.raises(OlpeError):
+        s.moments_accumulate()
+    chain = np.concatenate(parts, axis=1)               # [W, N, PS]
+    n, mean, m2 = s.moments()
+    assert n == chain.shape[1] == (201 - 20) // 3 + 1
+    ref_mean = chain.mean(axis=1)
+    ref_m2 = ((chain - ref_mean[:, None, :]) ** 2).sum(axis=1)
+    np.testing.assert_allclose(mean, ref_mean, rtol=1e-13)
+    np.testing.assert_allclose(m2, ref_m2, rtol=1e-10, atol=1e-300)
+    centre = ref_mean.mean(axis=0)
+    summ = s.moments_summary(centre)
+    ps, np_ = s.ps, s.np_
+    _, tries, acc = s.get_state()
+    assert summ[0] == n and summ[1] == W
+    np.testing.assert_allclose(summ[2:2 + ps], ref_mean.sum(axis=0), rtol=1e-13)
+    np.testing.assert_allclose(summ[2 + ps:2 + 2 * ps], ref_m2.sum(axis=0), rtol=1e-10)
+    np.testing.assert_allclose(summ[2 + 2 * ps:2 + 3 * ps],
+                               ((ref_mean - centre) ** 2).sum(axis=0), rtol=1e-9)
+    np.testing.assert_array_equal(summ[2 + 3 * ps:2 + 3 * ps + np_], tries.sum(axis=0))
+    np.testing.assert_array_equal(summ[2 + 3 * ps + np_:], acc.sum(axis=0))
+    # step 3's statistics from the moments equal step3.summary over the chains
+    got = step3.summary_from_moments(s.allreduce_moments(), nsrc=2)
+    ref = step3.summary(chain.transpose(1, 0, 2), nsrc=2)
+    for name, r in ref.items():
+        for key in ("mean", "std", "gr_psrf", "gr_rc"):
+            np.testing.assert_allclose(got[name][key], r[key], rtol=1e-12, err_msg=(name, key))
+    # checkpoint round trip, then one more launch continues the same accumulation
+    t = make_sampler(g, "fast")
+    t.seed(np.arange(70, 70 + W))
+    t.set_state(*s.get_state())
+    t.set_rng_state(*s.rng_state())
+    t.reset_count(s.count)
+    t.set_moments(n, mean, m2)
+    for x in (s, t):
+        x.run(30, burn_in=20, record_stride=3)
+        x.moments_accumulate()
+    for a, b in zip(s.moments(), t.moments()):
+        np.testing.assert_array_equal(a, b)

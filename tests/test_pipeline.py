@@ -218,3 +218,105 @@ def test_mpiexec_launch_like_the_reference(tmp_path, monkeypatch):
     image = str(tmp_path / "N2.20090531.29966.LDIF.fits")                  # never opened
     out = step2.main([image, "-q"], nsrc=2)
     assert out == str(tmp_path) + "/29966_apf_results/" and not os.path.exists(out)
+
+
+def test_native_chain_reader_equals_genfromtxt(tmp_path):
+    """step3.load_chains parses the chain files natively (olpe_csv_read_chains); the
+    values are np.genfromtxt's (the reference's reader, apf_step3.py:169-186) bit for
+    bit, including repr edge values, NaN / inf, subnormals and -0.0."""
+    rs = np.random.RandomState(3)
+    M, N, ps = 7, 45, 17
+    chains = rs.normal(size=(M, N, ps)) * 10.0 ** rs.randint(-320, 300, size=(M, N, ps))
+    chains[0, 3, :6] = [np.nan, np.inf, -np.inf, -0.0, 5e-324, 1e16]
+    chains[2, 7, :4] = [0.1 + 0.2, 1e-5, 123456789012345678.0, -2.2250738585072014e-308]
+    paths = [str(tmp_path / f"{w}_finalarray_mpi.csv") for w in range(M)]
+    pipeline.write_chain_csvs(paths, chains, nan_row=True)
+    for burn in (0, 1, 5):
+        got = step3.load_chains(str(tmp_path), M, additional_burnin=burn)
+        ref = np.stack([np.genfromtxt(p, delimiter=",") for p in paths], axis=1)[burn:]
+        assert got.shape == ref.shape == (N + 1 - burn, M, ps)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))   # bit for bit
+    for threads in (1, 3):
+        assert np.array_equal(step3.load_chains(str(tmp_path), M, threads=threads)[:, :, 1:],
+                              chains.transpose(1, 0, 2)[:, :, 1:])
+    # blank fields are missing values (NaN) and blank lines are skipped, as genfromtxt
+    with open(paths[1], "ab") as f:
+        f.write(b"\r\n")
+    with open(paths[4], "r+b") as f:
+        text = f.read().replace(b",", b", ", 3)
+        f.seek(0)
+        f.write(text)
+    got = step3.load_chains(str(tmp_path), M, additional_burnin=0)
+    ref = np.stack([np.genfromtxt(p, delimiter=",") for p in paths], axis=1)
+    assert np.array_equal(got, ref, equal_nan=True)
+    # shape errors name the file; garbage is an error, not a silent NaN
+    pipeline.write_chain_csv(paths[5], pipeline.with_seed_row(chains[5, :10]))
+    with pytest.raises(ValueError, match="5_finalarray_mpi.csv"):
+        step3.load_chains(str(tmp_path), M)
+    pipeline.write_chain_csvs(paths[5:6], chains[5:6], nan_row=True)
+    with open(paths[6], "r+b") as f:
+        f.seek(40)
+        f.write(b"x")
+    with pytest.raises(ValueError, match="not a number"):
+        step3.load_chains(str(tmp_path), M)
+
+
+def test_npy_sidecar_loader(tmp_path):
+    """load_chains(source="npy") reads the --npy sidecars (no NaN seed row: it counts as
+    the first additional_burnin row) to the same array as the CSV path."""
+    rs = np.random.RandomState(4)
+    M, N = 3, 20
+    chains = rs.normal(size=(M, N, 17))
+    paths = [str(tmp_path / f"{w}_finalarray_mpi.csv") for w in range(M)]
+    pipeline.write_chain_csvs(paths, chains, nan_row=True)
+    pipeline.append_npy_chains([str(tmp_path / f"{w}_chain.npy") for w in range(M)], chains, N, 0)
+    for burn in (1, 4):
+        assert np.array_equal(step3.load_chains(str(tmp_path), M, burn, source="npy"),
+                              step3.load_chains(str(tmp_path), M, burn))
+
+
+def _moments_vector(chains, centre=None):
+    """The olpe_moments_summary layout from chains [N, M, PS] on the host (two-pass)."""
+    N, M, ps = chains.shape
+    mean = chains.mean(axis=0)                                  # [M, PS]
+    m2 = ((chains - mean) ** 2).sum(axis=0)
+    c = mean.mean(axis=0) if centre is None else centre
+    out = np.zeros(5 * ps)
+    out[0], out[1] = N, M
+    out[2:2 + ps] = mean.sum(axis=0)
+    out[2 + ps:2 + 2 * ps] = m2.sum(axis=0)
+    out[2 + 2 * ps:2 + 3 * ps] = ((mean - c) ** 2).sum(axis=0)
+    out[2 + 3 * ps:2 + 4 * ps - 1] = 10.0
+    out[2 + 4 * ps - 1:] = 4.0
+    return out
+
+
+@pytest.mark.parametrize("nsrc", [2, 3])
+def test_summary_from_moments_equals_summary(golden, nsrc):
+    """The moment form of step 3's statistics (mean, std, GR PSRF / RC) equals
+    step3.summary over the chains (the reference's arithmetic, apf_step3.py:258-278) on
+    the hand-pinned GR fixture's chains.  Those are built to stress cancellation (a
+    column of mean -148.9 whose walkers' means differ by 1e-2): there both forms sit
+    within 1.2e-12 / 3.8e-12 of the fixture's exact rational PSRF, so the test asks
+    5e-12 of each against the exact values and of the two forms against each other
+    (1e-12 on real chains: tests/test_cli_gpu.py)."""
+    g = golden("gr")
+    tag = "2" if nsrc == 2 else "3"
+    chains = g["chains" + tag]
+    ref = step3.summary(chains, nsrc=nsrc)
+    got = step3.summary_from_moments(_moments_vector(chains), nsrc=nsrc)
+    for k, (name, r) in enumerate(ref.items()):
+        for key in ("mean", "std", "gr_psrf", "gr_rc"):
+            np.testing.assert_allclose(got[name][key], r[key], rtol=5e-12, err_msg=(name, key))
+        np.testing.assert_allclose(got[name]["gr_psrf"], g["psrf" + tag][k], rtol=5e-12)
+        np.testing.assert_allclose(got[name]["gr_rc"], g["rc" + tag][k], rtol=5e-12)
+        assert got[name]["acceptance"] == 0.4
+    # several contexts (step 2's --gpus shards) combine to the same vector
+    parts = [_moments_vector(chains[:, :2]), _moments_vector(chains[:, 2:])]
+    for p in parts:
+        p[2 + 2 * chains.shape[2]:2 + 3 * chains.shape[2]] = 0
+    centre = step3.pooled_mean(parts)
+    dev = [_moments_vector(chains[:, :2], centre), _moments_vector(chains[:, 2:], centre)]
+    comb = step3.combine_moments(parts, dev)
+    np.testing.assert_allclose(comb[2:], _moments_vector(chains)[2:] * np.r_[
+        np.ones(3 * chains.shape[2]), 2 * np.ones(2 * chains.shape[2] - 2)], rtol=1e-12)
