@@ -82,6 +82,7 @@ struct GibbsArgs {
   unsigned *uflag;     // [W]
   unsigned utag;       // this launch's tag base (a multiple of 16)
   unsigned *uerr;      // set to 1 when a hand-off wait times out (olpe_sync reports it)
+  unsigned long long wait_ticks;   // a hand-off wait gives up after this many 100 MHz ticks
   int balance;         // progress balancing of the LDS sampler (OLPE_BALANCE)
   int stagger;         // start offset per wave rank within a SIMD, in ~0.5 us (OLPE_STAGGER)
 };
@@ -193,8 +194,8 @@ __device__ __forceinline__ void st_coef(double *s, const Coef &k) {
 // cached deviate, done_at; the MT key words are agent-scope stores too), drains them
 // (s_waitcnt vmcnt(0)) and sets the flag with a relaxed agent store; the consumer polls
 // the flag with relaxed agent loads and takes one agent acquire before its loads.  The
-// poll ends after 30 s of real time (100 MHz s_memrealtime) whatever happens, so the
-// grid always drains.
+// poll ends after wait_ticks of real time (100 MHz s_memrealtime; the host sizes it to
+// the chunk: at least 30 s, launch_gibbs_t) whatever happens, so the grid always drains.
 // Write-through (sc1) stores of the handed-off words through global-address-space
 // pointers (never flat), so the hand-off needs no L2 write-back (release fence): the
 // guide's R1 form.  The same stores run at the end of every unit.
@@ -227,7 +228,8 @@ __device__ __forceinline__ void unit_publish(unsigned *flag, unsigned v, int lan
   if (lane == 0) __hip_atomic_store((gu32 *)flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigned *err,
-                                          unsigned long long *stats, int lane) {
+                                          unsigned long long *stats, int lane,
+                                          unsigned long long limit) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool waited = false;
   for (;;) {
@@ -235,7 +237,7 @@ __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigne
         (int)__hip_atomic_load((gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (v == want) break;
     waited = true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
       __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -387,7 +389,8 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       it_e = q * (k + 1) + (r * (k + 1)) / units;
       // the walker's previous chunk ran on another wave: wait for its hand-off
       if (k > 0 && active)
-        unit_wait(K()->uflag + w, K()->utag + (unsigned)k, K()->uerr, K()->queue + 2, lane);
+        unit_wait(K()->uflag + w, K()->utag + (unsigned)k, K()->uerr, K()->queue + 2, lane,
+                  K()->wait_ticks);
     }
     // ring sampler: the batch's waves run max(it_e - it_s) lockstep steps; a wave past
     // its own iterations (or without a unit) keeps the phase barriers (idle steps)
@@ -991,6 +994,15 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
                a.W <= (long long)resident * WPB) ? 1 : 0;
   c->last_units = q.units;
   if (q.units > 1) c->units_used = true;
+  // a hand-off waits at most for one chunk of the same walker (its predecessor) to run:
+  // bound a chunk's time generously -- 8 ns per pixel-Gaussian per iteration, ~30x the
+  // slowest sampler (EXACT, 3 sources, 128x128) -- and never below 30 s
+  {
+    const double chunk = (double)((a.n_iters + q.units - 1) / q.units);
+    const double ticks = chunk * (double)a.n * (double)a.n * (2.0 * NSRC) * 0.8;
+    q.wait_ticks = (unsigned long long)std::min(std::max(ticks, 3e9), 1e15);
+    c->wait_limit_s = (double)q.wait_ticks * 1e-8;
+  }
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
   // the launch takes W * units + (its waves) values off the counter (the ring sampler:
@@ -1334,7 +1346,9 @@ static int check_units(olpe_ctx *c) {
   if (!c->d_queue || !c->units_used) return OLPE_OK;   // (the word is sticky)
   unsigned long long e = 0;
   HIPCHK(hipMemcpy(&e, c->d_queue + 1, sizeof(e), hipMemcpyDeviceToHost));
-  if (e) return set_err(OLPE_EHIP, "sampler chunk hand-off timed out (30 s): results invalid");
+  if (e)
+    return set_err(OLPE_EHIP, "sampler chunk hand-off timed out (%.0f s): results invalid",
+                   c->wait_limit_s);
   return OLPE_OK;
 }
 
