@@ -254,6 +254,13 @@ __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigne
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#ifndef OLPE_RING_PRIO_STEP
+// A/B: the ring sampler's sweep priority by wave rank within a SIMD (younger waves ahead
+// of older ones; 0 = the hardware's age order, the default): 2 = priorities 0 / 1 / 2 for
+// waves 0-3 / 4-7 / 8-11 with the ring sampler's control chain at 3.  +0.5-0.8 % on one
+// box (profiles/r03/ab_c4_ring_window.log), +-0.3 % on the next (ab_c4_ring_prio.log)
+#define OLPE_RING_PRIO_STEP 0
+#endif
 #ifndef OLPE_CTRL_PRIO
 // wave priority of the step's control chain (the sweep runs at 0, or 0/1 with balancing)
 #define OLPE_CTRL_PRIO 2
@@ -464,7 +471,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
     ccache.colc = colc;
-    __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
+    __builtin_amdgcn_s_setprio(RING && OLPE_RING_PRIO_STEP > 1 ? 3 : OLPE_CTRL_PRIO);
 #ifdef OLPE_DIAG_TIMING
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long dt_last = __builtin_amdgcn_s_memtime();
@@ -612,6 +619,13 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         ++my_steps;
         if (behind) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
+      } else if (RING && OLPE_RING_PRIO_STEP) {
+        // A/B (OLPE_RING_PRIO_STEP = d): the ring sampler's lockstep waves sweep at
+        // priority (wave / 4) * d -- younger waves of a SIMD (wave, wave + 4, wave + 8)
+        // ahead of the older ones, against the hardware's age order
+        if ((wave >> 2) == 0) __builtin_amdgcn_s_setprio(0);
+        else if ((wave >> 2) == 1) __builtin_amdgcn_s_setprio(OLPE_RING_PRIO_STEP > 1 ? 1 : 0);
+        else __builtin_amdgcn_s_setprio(OLPE_RING_PRIO_STEP > 1 ? 2 : 1);
       } else {
         __builtin_amdgcn_s_setprio(0);
       }
@@ -624,7 +638,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
                                                        &hcache, &ccache, gmask, &gcache,
                                                        RING ? &ring : nullptr);
-      __builtin_amdgcn_s_setprio(OLPE_CTRL_PRIO);
+      __builtin_amdgcn_s_setprio(RING && OLPE_RING_PRIO_STEP > 1 ? 3 : OLPE_CTRL_PRIO);
       DT_MARK(3);
       // (the total is valid in lane 63: the accept ballots that lane's test, and lane 63
       // stores an accepted chi^2, so the step needs no readlanes of the sum)

@@ -1618,10 +1618,28 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // The DMA is issued from inline asm: the compiler then inserts no vmcnt(0) before the
 // issuing wave's next LDS reads (it cannot tell the ring slots apart), and its own
 // counted waits stay correct because vector memory operations retire in order.
+//
+// Windowed form (OLPE_RING_WINDOW, round 3): four slots of 16-row phases, the DMA of
+// phase g + 2 issued at the start of phase g, and no s_barrier per phase: a wave that
+// starts phase g first waits for its own DMAs and LDS reads (so it no longer reads phase
+// g - 1 and its DMA shares so far have landed), counts itself in with an LDS atomic
+// (arrive[g % 4]), and then waits only until every wave has started phase g - 1 --
+// which is when phase g's DMA (issued at g - 2) has landed everywhere and the slot of
+// phase g + 2 (phase g - 2's) is read by nobody.  The waves of a workgroup may so drift
+// one phase apart: the oldest wave of a SIMD runs into the next phase while the
+// younger ones finish, instead of idling at a barrier.
+#ifndef OLPE_RING_WINDOW
+#define OLPE_RING_WINDOW 0
+#endif
 template <int WAVES> struct LdsRing {
+#if OLPE_RING_WINDOW
+  static constexpr int ROWS = 16, SLOTS = 4, AHEAD = 2;
+#else
   static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
+  static constexpr int SLOTS = 2, AHEAD = 1;              // ring slots; DMA lead in phases
+#endif
   static constexpr int SLOT = ROWS * 64 * 16;
-  static constexpr int BYTES = 2 * SLOT;
+  static constexpr int BYTES = SLOTS * SLOT + (OLPE_RING_WINDOW ? 64 : 0);   // + counters
   static constexpr int PPP = 128 / ROWS;                  // phases per column pass
   static constexpr int PHASES = 2 * PPP;                  // phases per 128x128 sweep
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
@@ -1632,6 +1650,7 @@ template <int WAVES> struct LdsRing {
   unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
+  unsigned *arrive;      // windowed form: [SLOTS] arrival counters after the slots
 #ifdef OLPE_DIAG_TIMING
   // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
   // phase of a step (behind the workgroup's slowest control section) and at the others
@@ -1660,7 +1679,9 @@ template <int WAVES> struct LdsRing {
     for (int rr = 0; rr < ROWS; rr += WAVES)
       if (rr + wave < ROWS) dma_row(ph, sl, rr + wave);
   }
-  // before the first phase: phase 0 into slot 0
+  // before the first phase: phases 0 .. AHEAD-1 into their slots (the windowed form
+  // zeroes its counters too; the workgroup barrier of the first take_batch orders both
+  // before any wave's first phase)
   __device__ __forceinline__ void prologue(unsigned char *ring_lds, const double2 *dw, int w,
                                            int lane) {
     base = reinterpret_cast<const double2 *>(ring_lds);
@@ -1669,8 +1690,45 @@ template <int WAVES> struct LdsRing {
     wave = w;
     voff = (unsigned)lane * 16u;
     g = 0;
-    dma_phase(0, 0);
+    arrive = reinterpret_cast<unsigned *>(ring_lds + SLOTS * SLOT);
+    if (OLPE_RING_WINDOW && w == 0 && lane < SLOTS) arrive[lane] = 0u;
+#pragma unroll
+    for (int p = 0; p < AHEAD; ++p) dma_phase(p, p % SLOTS);
+    if (OLPE_RING_WINDOW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+#if OLPE_RING_WINDOW
+  // opens phase g (windowed form, above); returns phase g's slot
+  __device__ __forceinline__ const double2 *begin_phase() {
+#ifdef OLPE_DIAG_TIMING
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    typedef __attribute__((address_space(3))) unsigned lds_u32;
+    lds_u32 *cnt = (lds_u32 *)arrive;
+    if (voff == 0) __hip_atomic_fetch_add(cnt + g % SLOTS, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (g > 0) {
+      const unsigned p = g - 1;
+      const unsigned want = (unsigned)WAVES * (p / SLOTS + 1u);
+      for (;;) {
+        const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+            cnt + p % SLOTS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if ((int)(v - want) >= 0) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    asm volatile("" ::: "memory");
+#ifdef OLPE_DIAG_TIMING
+    const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t0;
+    if (g % PHASES == 0) wait_first += dtw;
+    else wait_rest += dtw;
+#endif
+    dma_phase((int)((g + AHEAD) % PHASES), (int)((g + AHEAD) % SLOTS));
+    const double2 *ph = base + (g % SLOTS) * (SLOT / 16);
+    ++g;
+    return ph;
+  }
+#else
   // the barrier that opens phase g; returns phase g's slot
   __device__ __forceinline__ const double2 *begin_phase() {
 #ifdef OLPE_DIAG_NO_BARRIER
@@ -1693,6 +1751,7 @@ template <int WAVES> struct LdsRing {
     ++g;
     return p;
   }
+#endif
   // a step without a sweep of this wave's own (idle wave, or a fallback sweep that read
   // the cutout from global memory): the phases' barriers and DMA shares only
   __device__ __forceinline__ void idle_step() {
