@@ -98,6 +98,29 @@ def work_per_step(n: int, nsrc: int, mode: str) -> float:
             + n * (EXP_TAB_OPS + 3) * 6 / np_)
 
 
+def mt_words_per_step(nsrc: int) -> float:
+    """MT19937 words one Gibbs iteration draws: randint(0, P) (one
+    word for P = 16; masked rejection, 32/19 words on average, for P = 19), the
+    proposal's gauss() (polar method: 4 words per attempt, accepted with probability
+    pi/4, two deviates per acceptance: 8/pi words per deviate) and accept_reject's
+    rand() (2 words)."""
+    return (1.0 if nsrc == 2 else 32.0 / 19.0) + 8.0 / np.pi + 2.0
+
+
+def algorithmic_bytes(W: int, nrec: int, iters: int, nsrc: int) -> dict:
+    """HBM bytes one sampler launch must move: the recorded chain rows,
+    every walker's state, counters and RNG scalars in and out, and the MT19937 state
+    advance -- each drawn word retires one key word, read and rewritten once per 624
+    draws (8 B per word)."""
+    ps = 17 if nsrc == 2 else 20
+    np_ = ps - 1
+    parts = {"chain_rows": W * nrec * ps * 8,
+             "state_counters_in_out": W * 2 * (ps * 8 + 2 * np_ * 4 + 24),
+             "mt_state_advance": W * iters * mt_words_per_step(nsrc) * 8}
+    parts["total"] = sum(parts.values())
+    return parts
+
+
 def sec8d_work(n: int, nsrc: int) -> float:
     """SURVEY.md §8(d)'s exp-form count Np*(12G+8) + E*Np*G (reference formula)."""
     g = 2 * nsrc
@@ -357,6 +380,10 @@ def main():
             out["equivalent_exp_form_rate"] = rate * algo / 1e12
             out["exp_form_work_per_walker_step"] = algo
             tb = traffic.get(key(mode), {}).get("bytes_per_launch") if default_shape else None
+            nrec = args.iters // args.stride if args.stride else 0
+            alg = algorithmic_bytes(wpg, nrec, args.iters, nsrc)
+            out["algorithmic_bytes"] = alg
+            out["traffic_over_algorithmic"] = tb / alg["total"] if tb else None
             out["traffic"] = tb
             out["hbm_gbs"] = tb / secs / 1e9 if tb else None
             out["hbm_frac"] = tb / secs / HBM_PEAK if tb else None
@@ -368,7 +395,8 @@ def main():
                 "SURVEY.md 8(d)'s exp-form count Np(12G+8) + E Np G (E = 16) at this rate, in T "
                 "lane-ops/s: FAST does far fewer operations, so it is no utilisation figure; "
                 "traffic = PMC FETCH_SIZE*2 + WRITE_SIZE bytes per launch "
-                "(profiles/pmc_traffic.json); the north star's >= 40 % HBM-read roofline does "
+                "(profiles/pmc_traffic.json), algorithmic_bytes = chain rows + walker state "
+                "in/out + the MT19937 state advance (8 B per drawn word); the north star's >= 40 % HBM-read roofline does "
                 "not apply to an LDS-resident FP64-VALU-bound kernel (SURVEY.md 8(d)): hbm_frac "
                 "is reported, not targeted")
             return out

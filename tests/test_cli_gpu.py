@@ -173,6 +173,17 @@ def test_cli_three_source_feeds_step3(tmp_path):
     assert list(s) == step3.NAMES_3[:-1]
     for name in s:
         assert s[name]["gr_rc"] == np.sqrt(s[name]["gr_psrf"]) or np.isnan(s[name]["gr_rc"])
+    # the device-moment summary of the 20-column chains (posterior_summary.json)
+    import json
+    with open(out + "posterior_summary.json") as f:
+        summ = json.load(f)
+    for name, r in s.items():
+        # (a parameter some walker never moved has a within-chain variance of exactly 0
+        # here and of NumPy's rounding of the mean otherwise: GR compared where every
+        # walker's chain varies)
+        moved = np.all(np.ptp(c[:, :, step3.NAMES_3.index(name)], axis=0) > 0)
+        for key in ("mean", "std") + (("gr_psrf", "gr_rc") if moved else ()):
+            np.testing.assert_allclose(summ[name][key], r[key], rtol=1e-12, err_msg=(name, key))
 
 
 @pytest.mark.parametrize("mode", ["iters", "accept_min"])
