@@ -1,5 +1,5 @@
 """bench.py's JSON contract, checked on CPU: the metric string is BASELINE.json's and the
-committed round-2 bench lines (profiles/r02/bench*.log, measured on an MI355X) carry
+committed round-3 bench lines (profiles/r03/bench*.log, measured on an MI355X) carry
 the fields the driver and the judge read (roofline with a fraction <= 1, cpu_baseline,
 a value consistent with the step time)."""
 import json
@@ -24,7 +24,7 @@ def test_metric_is_baselines():
 
 @pytest.mark.parametrize("name,cfg", [("bench", 2), ("bench_c1", 1), ("bench_c4", 4)])
 def test_committed_bench_lines(name, cfg):
-    d = _last_json(os.path.join(REPO, "profiles", "r02", f"{name}.log"))
+    d = _last_json(os.path.join(REPO, "profiles", "r03", f"{name}.log"))
     assert d["metric"] == bench.METRIC and d["unit"] == "walker-steps/s"
     assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["dtype"] == "f64" and d["vs_baseline"] is None
@@ -43,6 +43,13 @@ def test_committed_bench_lines(name, cfg):
     assert r["achieved"] == pytest.approx(r["frac"] * r["peak"], rel=1e-9)
     # the kernel's HIP-event time is the step time up to launch gaps (back-to-back queue)
     assert r["kernel_ms"] <= d["ms_per_step"] * 1.02
+    # the profiling session the counts come from (profiles/r03/roofline.json): the line's
+    # frac is the session's scaled by the box's speed, within a few per cent of it
+    p = r["profile"]
+    assert p["frac"] * p["frac_ratio_live_over_profile"] == pytest.approx(r["frac"], rel=1e-9)
+    assert abs(r["frac"] / p["frac"] - 1) < 0.03
+    assert r["algorithmic_bytes"]["total"] > 0 and 1 < r["traffic_over_algorithmic"] < 2
+    assert d["posterior"]["walkers"] == wpg and d["posterior"]["rows_per_walker"] > 0
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "walker-steps/s" and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["sample"]
