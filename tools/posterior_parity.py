@@ -70,6 +70,9 @@ def main():
     s.seed(seeds)
     s.set_state(np.tile(p0, (args.walkers, 1)))
     gpu = s.run(args.iters, burn_in=args.burn, record_stride=1)
+    s.moments_accumulate()
+    from olpefit_amd import step3
+    summ = step3.summary_from_moments(s.allreduce_moments(), nsrc)
     with mp.get_context("spawn").Pool(min(16, args.walkers)) as pool:
         ref = np.stack(pool.map(_oracle_walker, [(n, nsrc, int(sd), args.iters, args.burn)
                                                  for sd in seeds]))
@@ -90,6 +93,17 @@ def main():
         worst = max(worst, abs(mg - mr) / max(abs(mr), 1e-300))
         print(f"{name:>6} {truth[k]:12.6g} {mg:16.10g} {mr:16.10g} {abs(mg - mr):9.2e} "
               f"{sg:12.6g} {ds:14.2e}")
+    # step 3's statistics from the device moments (posterior_summary.json's numbers)
+    # against step 3's arithmetic over the oracle's chains
+    rs = step3.summary(ref.transpose(1, 0, 2), nsrc)
+    keys = list(rs)
+    dm = max(abs(summ[k]["mean"] - rs[k]["mean"]) / max(abs(rs[k]["mean"]), 1e-300) for k in keys)
+    dsd = max(abs(summ[k]["std"] - rs[k]["std"]) / max(rs[k]["std"], 1e-300) for k in keys)
+    dgr = max(abs(summ[k]["gr_rc"] - rs[k]["gr_rc"]) / rs[k]["gr_rc"] for k in keys)
+    dc = max(abs(summ[k]["mean"] - rs[k]["mean"]) for k in keys[:2 * nsrc])
+    print(f"device-moment summary vs step3.summary of the oracle chains: max relative "
+          f"|dmean| {dm:.2e}, |dsigma| {dsd:.2e}, |dGR RC| {dgr:.2e}; centroid |dmean| "
+          f"{dc:.2e} px")
     same = np.mean(np.isclose(gpu, ref, rtol=1e-8, atol=1e-9))
     print(f"max relative |dmean| {worst:.2e}; centroid |dmean| (px) "
           f"{max(abs(g[:, k].mean() - r[:, k].mean()) for k in range(2 * nsrc)):.2e}; "
