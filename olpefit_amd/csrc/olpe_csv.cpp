@@ -202,20 +202,6 @@ int olpe_csv_append_chains(const char *const *paths, const double *chains, int n
 // --- reader (apf_step3.py:169-186) -------------------------------------------------
 namespace {
 
-bool read_all(const char *path, std::vector<char> &buf) {
-  FILE *f = fopen(path, "rb");
-  if (!f) return false;
-  bool ok = fseek(f, 0, SEEK_END) == 0;
-  const long size = ok ? ftell(f) : -1;
-  ok = ok && size >= 0 && fseek(f, 0, SEEK_SET) == 0;
-  if (ok) {
-    buf.resize((size_t)size);
-    ok = fread(buf.data(), 1, (size_t)size, f) == (size_t)size;
-  }
-  fclose(f);
-  return ok;
-}
-
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
 // one field as np.genfromtxt's float converter reads it: surrounding blanks stripped, an
@@ -237,16 +223,49 @@ bool blank(const char *a, const char *b) {
   return a == b;
 }
 
-// the lines of buf (without the terminator); blank lines are skipped, as genfromtxt does
-template <class F> bool for_lines(const std::vector<char> &buf, F &&fn) {
-  const char *p = buf.data(), *end = p + buf.size();
-  while (p < end) {
-    const char *eol = (const char *)memchr(p, '\n', (size_t)(end - p));
-    if (!eol) eol = end;
-    if (!blank(p, eol) && !fn(p, eol)) return false;
-    p = eol + 1;
+// The lines of a file (without the terminator), read in blocks of 4 MiB so that a long
+// chain file (the reference's accept_min run records ~1.6 M rows, ~0.5 GB) never sits
+// in memory whole; blank lines are skipped, as genfromtxt does.  Returns 1 when every
+// line was handed to fn, 0 when fn stopped, -1 on a read error.
+template <class F> int for_file_lines(const char *path, F &&fn) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return -1;
+  constexpr size_t kBlock = (size_t)1 << 22;
+  std::vector<char> buf;
+  size_t have = 0;             // a partial line carried over from the previous block
+  int rc = 1;
+  for (;;) {
+    if (buf.size() < have + kBlock) buf.resize(have + kBlock);
+    const size_t got = fread(buf.data() + have, 1, kBlock, f);
+    if (got < kBlock && ferror(f)) {
+      rc = -1;
+      break;
+    }
+    const bool eof = got < kBlock;
+    const char *p = buf.data(), *end = p + have + got;
+    bool stop = false;
+    for (;;) {
+      const char *eol = (const char *)memchr(p, '\n', (size_t)(end - p));
+      if (!eol) break;
+      if (!blank(p, eol) && !fn(p, eol)) {
+        stop = true;
+        break;
+      }
+      p = eol + 1;
+    }
+    if (stop) {
+      rc = 0;
+      break;
+    }
+    if (eof) {                 // a last line without a terminator
+      if (p < end && !blank(p, end) && !fn(p, end)) rc = 0;
+      break;
+    }
+    have = (size_t)(end - p);
+    memmove(buf.data(), p, have);
   }
-  return true;
+  fclose(f);
+  return rc;
 }
 
 }  // namespace
@@ -255,17 +274,16 @@ extern "C" {
 
 int olpe_csv_shape(const char *path, long long *rows, int *cols) {
   if (!path || !rows || !cols) return olpe::set_err(OLPE_EINVAL, "olpe_csv_shape: NULL argument");
-  std::vector<char> buf;
-  if (!read_all(path, buf)) return olpe::set_err(OLPE_EIO, "olpe_csv_shape: cannot read %s", path);
   long long n = 0;
   int c = 0;
-  for_lines(buf, [&](const char *a, const char *b) {
+  const int rc = for_file_lines(path, [&](const char *a, const char *b) {
     if (n++ == 0) {
       c = 1;
       for (const char *q = a; q < b; ++q) c += *q == ',';
     }
     return true;
   });
+  if (rc < 0) return olpe::set_err(OLPE_EIO, "olpe_csv_shape: cannot read %s", path);
   *rows = n;
   *cols = c;
   return OLPE_OK;
@@ -286,16 +304,10 @@ int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, 
   std::vector<int> failed(nt, -1);
   std::vector<std::string> why(nt);
   auto work = [&](unsigned t) {
-    std::vector<char> buf;
     char msg[160];
     for (int i = (int)t; i < nfiles; i += (int)nt) {
-      if (!read_all(paths[i], buf)) {
-        failed[t] = i;
-        why[t] = "cannot read";
-        return;
-      }
       long long row = 0;
-      const bool ok = for_lines(buf, [&](const char *a, const char *b) {
+      const int frc = for_file_lines(paths[i], [&](const char *a, const char *b) {
         if (row >= nrows) {
           snprintf(msg, sizeof(msg), "more than %lld rows (walker 0's length)", nrows);
           return false;
@@ -328,8 +340,13 @@ int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, 
         ++row;
         return true;
       });
-      if (ok && row != nrows) snprintf(msg, sizeof(msg), "%lld rows, not %lld", row, nrows);
-      if (!ok || row != nrows) {
+      if (frc < 0) {
+        failed[t] = i;
+        why[t] = "cannot read";
+        return;
+      }
+      if (frc > 0 && row != nrows) snprintf(msg, sizeof(msg), "%lld rows, not %lld", row, nrows);
+      if (frc == 0 || row != nrows) {
         failed[t] = i;
         why[t] = msg;
         return;
@@ -342,7 +359,7 @@ int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, 
   for (auto &th : pool) th.join();
   for (unsigned t = 0; t < nt; ++t)
     if (failed[t] >= 0)
-      return olpe::set_err(failed[t] >= 0 && why[t] == "cannot read" ? OLPE_EIO : OLPE_EINVAL,
+      return olpe::set_err(why[t] == "cannot read" ? OLPE_EIO : OLPE_EINVAL,
                            "olpe_csv_read_chains: %s: %s", paths[failed[t]], why[t].c_str());
   return OLPE_OK;
 }

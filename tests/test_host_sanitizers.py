@@ -3,7 +3,8 @@
 the parity tests and tests/test_kernel_resources.py instead).
 
 olpe_csv.cpp -- the chain-file writer (repr-exact formatting, one file per walker from
-a pool of threads, append mode for the streamed CLI) -- is built with g++
+a pool of threads, append mode for the streamed CLI) and the step-3 reader (block-wise
+threaded parser) -- is built with g++
 -fsanitize=address,undefined into a small driver and run over edge values (signed zero,
 subnormals, the largest double, the repr fixed/scientific boundaries, non-finite values)
 and a threaded write + append of many files.  Any sanitizer report aborts the driver;
@@ -32,6 +33,8 @@ int set_err(int code, const char *, ...) { return code; }   // (libolpe's lives 
 // fmt <hex doubles...>: one row, formatted with a NaN row first
 // files <dir> <nfiles> <nrows> <ncols> <threads>: write (NaN row + rows), append rows,
 //   values from a fixed LCG bit pattern, sizes printed
+// read <dir> <nfiles> <nrows> <ncols> <threads>: write, then read back through the
+//   step-3 reader (olpe_csv_read_chains) and compare the bits
 static double bits(unsigned long long u) { double d; __builtin_memcpy(&d, &u, 8); return d; }
 int main(int argc, char **argv) {
   const std::string mode = argv[1];
@@ -58,6 +61,25 @@ int main(int argc, char **argv) {
     d = bits((x >> 2) | 0x3000000000000000ull) * ((x & 1) ? -1.0 : 1.0);
   }
   if (olpe_csv_write_chains(paths.data(), ch.data(), nf, nr, nc, 1, th)) return 4;
+  if (mode == "read") {       // step 3's read of the same files, compared bit for bit
+    long long rows = 0;
+    int cols = 0;
+    if (olpe_csv_shape(paths[0], &rows, &cols) || rows != nr + 1 || cols != nc) return 7;
+    std::vector<double> back((size_t)nr * nf * nc);
+    if (olpe_csv_read_chains(paths.data(), nf, rows, cols, 1, back.data(), th)) return 8;
+    for (int i = 0; i < nf; ++i)
+      for (int r = 0; r < nr; ++r)
+        for (int c = 0; c < nc; ++c)
+          if (__builtin_memcmp(&back[((size_t)r * nf + i) * nc + c],
+                               &ch[((size_t)i * nr + r) * nc + c], 8))
+            return 9;
+    // a file with one row too many is an error naming it, not a crash
+    if (olpe_csv_append_chains(paths.data(), ch.data(), 1, nr, 1, nc, 1, nullptr)) return 10;
+    if (olpe_csv_read_chains(paths.data(), nf, rows, cols, 1, back.data(), th) != OLPE_EINVAL)
+      return 11;
+    printf("read ok\n");
+    return 0;
+  }
   std::vector<long long> sz(nf);
   if (olpe_csv_append_chains(paths.data(), ch.data(), nf, nr, nr / 2, nc, th, sz.data())) return 5;
   for (int i = 0; i < nf; ++i) printf("%lld\n", sz[i]);
@@ -136,3 +158,10 @@ def test_threaded_write_and_append_under_sanitizers(driver, tmp_path):
         body = lines[1:-1]
         assert len(body) == nr + nr // 2 and body[nr:] == body[:nr // 2]
         assert all(len(l.split(",")) == nc for l in body)
+
+
+@pytest.mark.parametrize("nf,nr", [(9, 40), (2, 20000)])
+def test_threaded_reader_under_sanitizers(driver, tmp_path, nf, nr):
+    """The reader parses in 4 MiB blocks: 2 x 20,000-row files (~8 MB each) carry lines
+    across block ends; values come back bit for bit, a file of another length is an error."""
+    assert _run(driver, "read", str(tmp_path), str(nf), str(nr), "17", "3").strip() == "read ok"
