@@ -1211,6 +1211,15 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
       hDW[i] = make_double2(d * (1.0 / e), 1.0 / e);
     }
   }
+  // an all-masked cutout: the reference's masked sum is np.ma.masked, which :289 stores
+  // as NaN and :144 never accepts (bool(masked) is False); one NaN pixel gives every chi^2
+  // that NaN (an empty sum here would be 0 and accept every proposal)
+  bool any_pixel = false;
+  for (size_t i = 0; i < npix && !any_pixel; ++i) any_pixel = hDE[i].y != 0.0;
+  if (!any_pixel) {
+    hDE[0] = make_double2(NAN, NAN);
+    hDW[0] = make_double2(NAN, NAN);
+  }
   int rc;
   hipError_t e1 = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e1 != hipSuccess) {

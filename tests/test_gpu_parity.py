@@ -160,6 +160,39 @@ def test_nonfinite_pixels_dropped_by_the_library(golden, lib_loaded, name, mode)
     np.testing.assert_allclose(chi, g["chi2"], rtol=TOL[mode]["chi"])
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("fill", ["nan", "saturated"])
+def test_all_masked_cutout_rejects_everything(golden, lib_loaded, mode, fill):
+    """A cutout with no usable pixel (all NaN, or all above the saturation mask): the
+    reference's np.ma sum is np.ma.masked, stored as NaN (apf_step2.py:289) and never
+    accepted (:144); chi^2 is NaN here too and the trajectory (index, dice, no accept)
+    equals the oracle's."""
+    g = golden("c32")
+    img = np.full((32, 32), np.nan if fill == "nan" else 1e6, np.float32)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = g["p_init"].copy()
+    with np.errstate(all="ignore"):
+        w = ora.Walker(dm, err, p0, 17)
+        w.init_chi2()
+    assert np.isnan(w.parameters[-1])
+    from olpefit_amd.core import Sampler
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+    s.set_eval_mode(mode)
+    assert np.isnan(s.chi_squared(p0))
+    p0[-1] = np.nan
+    s.seed([17])
+    s.set_state(p0[None])
+    s.enable_trace(True)
+    chain = s.run(60, record_stride=1)
+    tr = s.trace(60)
+    with np.errstate(all="ignore"):
+        ref, rtr = w.run(60, trace=True)
+    np.testing.assert_array_equal(tr[0, :, 0].astype(int), [t[0] for t in rtr])
+    np.testing.assert_array_equal(tr[0, :, 3], [t[3] for t in rtr])
+    assert not np.any(tr[0, :, 5]) and not any(t[4] for t in rtr)
+    np.testing.assert_array_equal(chain[0], ref)
+
+
 @pytest.mark.parametrize("name", ["c32", "c64_3"])
 def test_accept_min_done_at(golden, lib_loaded, name):
     """The reference loop ran until min(total_tries) >= accept_min (apf_step2.py:300):
@@ -692,11 +725,12 @@ def test_work_units_automatic_choice(lib_loaded, monkeypatch):
 @pytest.mark.parametrize("n,nsrc,mode", [(40, 2, "fast"), (40, 2, "exact"), (48, 3, "fast"),
                                          (80, 2, "fast"), (96, 3, "fast"), (128, 2, "fast"),
                                          (24, 2, "fast"), (32, 3, "fast"), (32, 3, "exact"),
-                                         (64, 3, "fast")])
+                                         (64, 3, "fast"), (256, 2, "fast"), (256, 3, "exact")])
 def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
     """Cutout sides without a dedicated kernel (runtime-n LDS sampler for n <= ~72,
-    global-memory sampler above; 128 with two sources; n < 32 with several row groups
-    per wave, n not dividing 64) and the 3-source 32x32 / 64x64 kernels on synthetic
+    global-memory sampler above; 128 with two sources; 256, where the FAST3 guard fails
+    on the whole grid; n < 32 with several row groups per wave, n not dividing 64) and
+    the 3-source 32x32 / 64x64 kernels on synthetic
     frames: model, chi^2 and 3 walkers x 300 iterations against the oracle."""
     from olpefit_amd import synth
     from olpefit_amd.core import Sampler
