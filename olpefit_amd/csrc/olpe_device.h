@@ -1650,7 +1650,9 @@ template <int WAVES> struct LdsRing {
   unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
+#if OLPE_RING_WINDOW
   unsigned *arrive;      // windowed form: [SLOTS] arrival counters after the slots
+#endif
 #ifdef OLPE_DIAG_TIMING
   // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
   // phase of a step (behind the workgroup's slowest control section) and at the others
@@ -1690,11 +1692,15 @@ template <int WAVES> struct LdsRing {
     wave = w;
     voff = (unsigned)lane * 16u;
     g = 0;
+#if OLPE_RING_WINDOW
     arrive = reinterpret_cast<unsigned *>(ring_lds + SLOTS * SLOT);
-    if (OLPE_RING_WINDOW && w == 0 && lane < SLOTS) arrive[lane] = 0u;
+    if (w == 0 && lane < SLOTS) arrive[lane] = 0u;
 #pragma unroll
     for (int p = 0; p < AHEAD; ++p) dma_phase(p, p % SLOTS);
-    if (OLPE_RING_WINDOW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    dma_phase(0, 0);
+#endif
   }
 #if OLPE_RING_WINDOW
   // opens phase g (windowed form, above); returns phase g's slot
