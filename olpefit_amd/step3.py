@@ -34,13 +34,16 @@ def load_chains(input_directory: str, ncor: int, additional_burnin: int = 1,
         paths = [os.path.join(input_directory, f"{i}_chain.npy") for i in range(ncor)]
         first = np.load(paths[0], mmap_mode="r")
         length, ps = first.shape[0] + 1, first.shape[1]
-        out = np.empty((max(0, length - additional_burnin), ncor, ps))
-        lo = max(0, additional_burnin - 1)
+        burn = min(max(0, int(additional_burnin)), length)
+        out = np.empty((length - burn, ncor, ps))
+        if burn == 0:
+            out[0] = np.nan                     # the seed row the CSV files start with
+        lo, o = max(0, burn - 1), 1 if burn == 0 else 0
         for i, p in enumerate(paths):
             a = np.load(p, mmap_mode="r")
             if a.shape != first.shape:
                 raise ValueError(f"walker {i}: chain shape {a.shape} != walker 0's {first.shape}")
-            out[:, i, :] = a[lo:]
+            out[o:, i, :] = a[lo:]
         return out
     if source != "csv":
         raise ValueError("source must be 'csv' or 'npy'")

@@ -270,9 +270,9 @@ def test_npy_sidecar_loader(tmp_path):
     paths = [str(tmp_path / f"{w}_finalarray_mpi.csv") for w in range(M)]
     pipeline.write_chain_csvs(paths, chains, nan_row=True)
     pipeline.append_npy_chains([str(tmp_path / f"{w}_chain.npy") for w in range(M)], chains, N, 0)
-    for burn in (1, 4):
+    for burn in (0, 1, 4, N + 1):
         assert np.array_equal(step3.load_chains(str(tmp_path), M, burn, source="npy"),
-                              step3.load_chains(str(tmp_path), M, burn))
+                              step3.load_chains(str(tmp_path), M, burn), equal_nan=True)
 
 
 def _moments_vector(chains, centre=None):
