@@ -40,7 +40,7 @@ import time
 
 import numpy as np
 
-from . import _lib, fitsio, pipeline, step3
+from . import _lib, dist, fitsio, pipeline, step3
 from .core import Sampler
 
 MAX_CHUNK = 20000          # iterations per launch when memory allows
@@ -111,6 +111,9 @@ def parse(argv, nsrc, variant="2"):
                     help="also write one every N launches (0 = only by time)")
     ap.add_argument("--resume", action="store_true",
                     help="continue the run recorded in the output directory's checkpoint")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="one process per rank (torchrun): every rank on --device instead "
+                         "of LOCAL_RANK's GPUs (a rehearsal on a one-GPU host)")
     ap.add_argument("--no-csv", action="store_true")
     ap.add_argument("--npy", action="store_true", help="also write {w}_chain.npy")
     ap.add_argument("-q", "--quiet", action="store_true")
@@ -199,8 +202,10 @@ class Output:
     """The per-walker files of one run: chain CSVs (+ optional .npy sidecars) grown by
     each launch, acceptance files rewritten at each launch, and the checkpoint."""
 
-    def __init__(self, outdir, shards, variant, csv, npy):
+    def __init__(self, outdir, shards, variant, csv, npy, base=0):
+        # base: the process's first global walker (checkpoint arrays are indexed from it)
         self.outdir, self.shards, self.csv, self.npy = outdir, shards, csv, npy
+        self.base = base
         if variant == "2":
             self.names = [[(f"{sh.w0 + k}_finalarray_mpi.csv", f"{sh.w0 + k}_acceptance_rate.csv")
                            for k in range(sh.W)] for sh in shards]
@@ -229,16 +234,17 @@ class Output:
         A file shorter than the checkpoint recorded is not this run's: refused (a
         truncate would pad it with NUL bytes)."""
         for g, sh in enumerate(self.shards):
+            mine = sizes[sh.w0 - self.base:sh.w0 - self.base + sh.W]
             if self.csv:
-                for p, n in zip(self._paths(g, 0), sizes[sh.w0:sh.w0 + sh.W]):
+                for p, n in zip(self._paths(g, 0), mine):
                     have = os.path.getsize(p) if os.path.exists(p) else -1
                     if have < int(n):
                         raise ValueError(f"--resume: {p} holds {have} bytes, fewer than the "
                                          f"{int(n)} the checkpoint recorded: not this run's file")
-                for p, n in zip(self._paths(g, 0), sizes[sh.w0:sh.w0 + sh.W]):
+                for p, n in zip(self._paths(g, 0), mine):
                     with open(p, "r+b") as f:
                         f.truncate(int(n))
-                self.sizes[g] = np.array(sizes[sh.w0:sh.w0 + sh.W], dtype=np.int64)
+                self.sizes[g] = np.array(mine, dtype=np.int64)
         if self.npy:
             for g, sh in enumerate(self.shards):
                 pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
@@ -278,7 +284,9 @@ class Output:
         return np.concatenate(self.sizes)
 
 
-def checkpoint_path(outdir, variant):
+def checkpoint_path(outdir, variant, rank=0, world=1):
+    if world > 1:        # one per rank of a multi-process run (its walkers only)
+        return outdir + f"step2_checkpoint.rank{rank}of{world}.npz"
     return outdir + ("step2_checkpoint.npz" if variant == "2" else "step2a_checkpoint.npz")
 
 
@@ -309,12 +317,19 @@ def run_id_path(outdir, variant):
     return outdir + ("step2_run_id" if variant == "2" else "step2a_run_id")
 
 
-def posterior_summary(shards, nsrc):
+def posterior_summary(shards, nsrc, group=None):
     """step3.summary_from_moments over every shard's walkers (two passes: the pooled
-    mean, then the walkers' deviations about it)."""
-    parts = [sh.s.moments_summary() for sh in shards]
+    mean, then the walkers' deviations about it); with a host group, over every rank's
+    shards (the vectors are 2 + 3 PS + 2 P doubles: gathered over TCP, exact in JSON)."""
+    def everywhere(vecs):
+        vecs = [np.asarray(v, dtype=np.float64) for v in vecs]
+        if group is None or group.world <= 1:
+            return vecs
+        return [np.asarray(v) for part in group.allgather([v.tolist() for v in vecs])
+                for v in part]
+    parts = everywhere([sh.s.moments_summary() for sh in shards])
     centre = step3.pooled_mean(parts)
-    dev = [sh.s.moments_summary(centre) for sh in shards]
+    dev = everywhere([sh.s.moments_summary(centre) for sh in shards])
     return step3.summary_from_moments(step3.combine_moments(parts, dev), nsrc)
 
 
@@ -323,7 +338,15 @@ def main(argv=None, nsrc=2, variant="2"):
     walker warm-up of apf_step2a.py writing step2a.csv / step2a_acceptance_rate
     (:320-331), which ``apf_step2.py -i 2a`` then starts from (apf_step2.py:248-256)."""
     args = parse(sys.argv[1:] if argv is None else argv, nsrc, variant)
-    say = (lambda *a: None) if args.quiet else print
+    # one process per GPU under torchrun (RANK / WORLD_SIZE / LOCAL_RANK): rank r runs
+    # walkers [r W / N, (r+1) W / N) and writes their files; ranks agree through the
+    # stdlib-TCP host group on the seed base, the run id, the launch length, the
+    # accept_min stop and the checkpoints, and sum their moments for the summary
+    rank, world, local = dist.env()
+    if variant != "2" or args.mpi_size > 1 or "LOCAL_RANK" not in os.environ:
+        rank, world, local = 0, 1, 0
+    group = dist.HostGroup(rank, world) if world > 1 else None
+    say = (lambda *a: None) if (args.quiet or rank > 0) else print
     if args.mpi_rank > 0:
         # an mpiexec launch: rank 0 runs every walker (see MPI_ENV)
         say(f"MPI rank {args.mpi_rank} of {args.mpi_size}: rank 0 runs all "
@@ -333,16 +356,18 @@ def main(argv=None, nsrc=2, variant="2"):
     directory, frame, outdir = pipeline.image_paths(args.image)  # :164-170
     say(outdir)
     os.makedirs(outdir, exist_ok=True)                           # :172-173
-    ckpt = checkpoint_path(outdir, variant)
+    ckpt = checkpoint_path(outdir, variant, rank, world)
     resume = load_checkpoint(ckpt) if args.resume else None
     if args.resume and resume is None:
         raise FileNotFoundError(ckpt)
     config = {"image": os.path.abspath(args.image), "nsrc": nsrc, "variant": variant,
               "walkers": args.walkers, "accept_min": args.accept_min, "burn_in": args.burn_in,
               "iters": args.iters, "stride": args.record_stride, "exact": args.exact,
-              "fixed_bkgd": args.fixed_bkgd, "csv": not args.no_csv, "npy": args.npy}
+              "fixed_bkgd": args.fixed_bkgd, "csv": not args.no_csv, "npy": args.npy,
+              "ranks": world}
     if resume is not None:
         old = json.loads(str(resume["config"]))
+        old.setdefault("ranks", 1)
         base, p0, run_id = old.pop("seed"), np.array(old.pop("p0")), old.pop("run_id", None)
         try:
             with open(run_id_path(outdir, variant)) as f:
@@ -367,28 +392,37 @@ def main(argv=None, nsrc=2, variant="2"):
             p0 = pipeline.initial_parameters(image, guess, nsrc)
         base = args.seed if args.seed is not None else int.from_bytes(os.urandom(4), "little")
         run_id = os.urandom(8).hex()
+        if group is not None:
+            base, run_id = group.broadcast([base, run_id])        # rank 0's
     config.update(seed=base, p0=[float(v) for v in p0], run_id=run_id)
     W = args.walkers
     seeds = (base + np.arange(W, dtype=np.int64)) & 0xFFFFFFFF
-    say(f"walkers {W}, seeds {base}..{base + W - 1} (np.random.seed semantics)")
-    ng = max(1, min(args.gpus, W))
-    bounds = [(g * W) // ng for g in range(ng + 1)]
-    shards = [Shard(image, hdr, nsrc, args.device + g, bounds[g], bounds[g + 1] - bounds[g], p0,
+    say(f"walkers {W}, seeds {base}..{base + W - 1} (np.random.seed semantics)"
+        + (f", {world} ranks" if world > 1 else ""))
+    pw0, pW = dist.shard(W, world, rank)              # this process's walkers
+    if pW < 1:
+        raise ValueError(f"{W} walkers over {world} ranks: rank {rank} has none")
+    ng = max(1, min(args.gpus, pW))
+    dev0 = args.device + (0 if args.share_gpu else local * ng)
+    bounds = [pw0 + (g * pW) // ng for g in range(ng + 1)]
+    shards = [Shard(image, hdr, nsrc, dev0 + g, bounds[g], bounds[g + 1] - bounds[g], p0,
                     seeds, args.exact, 1 if args.fixed_bkgd else 0) for g in range(ng)]
     say("Found initial chi-squared:", shards[0].p_init[-1])
     say("Initial guess:", shards[0].p_init)
 
-    out = Output(outdir, shards, variant, csv=not args.no_csv, npy=args.npy)
+    out = Output(outdir, shards, variant, csv=not args.no_csv, npy=args.npy, base=pw0)
     count = 0
     if resume is not None:
         count = int(resume["count"])
+        if group is not None and len(set(group.allgather(count))) != 1:
+            raise ValueError("--resume: the ranks' checkpoints are at different counts")
         for sh in shards:
-            sl = slice(sh.w0, sh.w0 + sh.W)
+            sl = slice(sh.w0 - pw0, sh.w0 - pw0 + sh.W)
             sh.restore(((resume["state"][sl], resume["tries"][sl], resume["accepts"][sl]),
                         (resume["mt"][sl], resume["gauss"][sl]), count))
         if "mom_n" in resume:
             for sh in shards:
-                sl = slice(sh.w0, sh.w0 + sh.W)
+                sl = slice(sh.w0 - pw0, sh.w0 - pw0 + sh.W)
                 sh.s.set_moments(int(resume["mom_n"]), resume["mom_mean"][sl],
                                  resume["mom_m2"][sl])
         out.truncate(resume["csv_sizes"], int(resume["npy_rows"]))
@@ -397,24 +431,30 @@ def main(argv=None, nsrc=2, variant="2"):
         # resumable against the files rewritten now
         if os.path.exists(ckpt):
             os.remove(ckpt)
-        with open(run_id_path(outdir, variant), "w") as f:
-            f.write(run_id + "\n")
+        if rank == 0:
+            with open(run_id_path(outdir, variant), "w") as f:
+                f.write(run_id + "\n")
         out.start()
 
     burn, stride = args.burn_in, args.record_stride
     chunk = chunk_size(shards, stride, args.chunk, args.mem_budget)
+    if group is not None:                 # every rank launches the same iterations
+        chunk = int(-group.allmax(-chunk))
     launches = 0
     last_ckpt = time.monotonic()
 
     def commit():
         # checkpoints are spaced by time (and optionally by launches), not written per
-        # launch: one holds every walker's MT key (190 MB at 65,536 walkers)
+        # launch: one holds every walker's MT key (190 MB at 65,536 walkers).  Rank 0's
+        # clock decides for every rank, so that all checkpoints hold the same count.
         nonlocal launches, last_ckpt
         out.commit(acceptance=count >= burn)
         launches += 1
         now = time.monotonic()
-        due = (args.checkpoint_every and launches % args.checkpoint_every == 0) or \
-              (args.checkpoint_secs > 0 and now - last_ckpt >= args.checkpoint_secs)
+        due = bool((args.checkpoint_every and launches % args.checkpoint_every == 0) or
+                   (args.checkpoint_secs > 0 and now - last_ckpt >= args.checkpoint_secs))
+        if group is not None:
+            due = bool(group.broadcast(due))
         if due:
             save_checkpoint(ckpt, shards, out, count, config)
             last_ckpt = time.monotonic()
@@ -445,6 +485,9 @@ def main(argv=None, nsrc=2, variant="2"):
             run(chunk, args.accept_min)
             hits = np.concatenate([sh.s.done_at() for sh in shards])
             hits = hits[hits >= 0]
+            if group is not None:         # the earliest hit over every rank's walkers
+                first = group.allmax(-float(hits.min()) if hits.size else -np.inf)
+                hits = np.array([int(-first)]) if np.isfinite(first) else hits[:0]
             if not hits.size:
                 count += chunk
                 commit()
@@ -460,9 +503,10 @@ def main(argv=None, nsrc=2, variant="2"):
             say("Loop count:", count)
             break
     if variant == "2":
-        summ = posterior_summary(shards, nsrc)
-        with open(outdir + "posterior_summary.json", "w") as f:
-            json.dump(summ, f, indent=1)
+        summ = posterior_summary(shards, nsrc, group)
+        if rank == 0:
+            with open(outdir + "posterior_summary.json", "w") as f:
+                json.dump(summ, f, indent=1)
         if summ["_rows_per_walker"] > 1:
             say("Posterior (device moments):", {k: round(summ[k]["mean"], 6)
                                                 for k in list(summ)[:4]})
@@ -470,5 +514,8 @@ def main(argv=None, nsrc=2, variant="2"):
         os.remove(ckpt)                  # the run is complete: nothing to resume
     for sh in shards:
         sh.s.close()
+    if group is not None:
+        group.barrier()                   # every rank's files are complete
+        group.close()
     say("done with loop")
     return outdir

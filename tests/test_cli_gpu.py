@@ -350,3 +350,50 @@ def test_cli_resume_refuses_another_runs_files(tmp_path, monkeypatch):
         f.truncate(10)
     with pytest.raises(ValueError, match="fewer than"):
         step2.main([path, *run, "--resume"])
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("mode", ["iters", "accept_min"])
+def test_cli_torchrun_ranks_equal_one_process(tmp_path, mode):
+    """apf_step2 launched one process per GPU (torchrun; here 2 ranks sharing the one
+    GPU, --share-gpu): each rank runs its contiguous walker range and writes its walkers'
+    files; the ranks agree on the launch length, the accept_min stop (the earliest hit
+    over every rank, apf_step2.py:300 + the barrier at :338) and the summary.  Every file
+    equals a one-process run's byte for byte; the posterior summary (moments summed over
+    the ranks) equals it to rtol 1e-12."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["--walkers", "7", "--seed", "31", "--burn-in", "20", "--chunk", "60", "-q", "--npy",
+            "--checkpoint-every", "2"]
+    args += ["--iters", "230"] if mode == "iters" else ["--accept-min", "30"]
+    one = step2.main([synth.write_case(str(tmp_path / "one"), 32, 2), *args])
+    path2 = synth.write_case(str(tmp_path / "two"), 32, 2)
+    env = dict(os.environ)
+    for k in [k for pair in step2.MPI_ENV for k in pair]:
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_free_port()), "apf_step2.py", path2, *args,
+                        "--share-gpu"], cwd=repo, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = pipeline.image_paths(path2)[2]
+    for w in range(7):
+        for name in (f"{w}_finalarray_mpi.csv", f"{w}_acceptance_rate.csv"):
+            with open(one + name, "rb") as f, open(two + name, "rb") as g:
+                assert f.read() == g.read(), name
+        np.testing.assert_array_equal(np.load(two + f"{w}_chain.npy"), np.load(one + f"{w}_chain.npy"))
+    with open(one + "posterior_summary.json") as f, open(two + "posterior_summary.json") as g:
+        a, b = json.load(f), json.load(g)
+    for name in step3.NAMES_2[:-1]:
+        for key in ("mean", "std", "gr_psrf", "gr_rc", "tries", "accepts"):
+            np.testing.assert_allclose(b[name][key], a[name][key], rtol=1e-12, err_msg=(name, key))
+    assert not [f for f in os.listdir(two) if "checkpoint" in f]
