@@ -81,7 +81,27 @@ def test_null_arguments_are_errors(lib):
     assert lib.olpe_model(None, None, None) == _lib.EINVAL
     assert lib.olpe_run(None, 1, 0, 1, 0, None) == _lib.EINVAL
     assert lib.olpe_sync(None) == _lib.EINVAL
+    assert lib.olpe_moments_accumulate(None) == _lib.EINVAL
+    assert lib.olpe_moments_reset(None) == _lib.EINVAL
+    assert lib.olpe_moments_get(None, None, None, None) == _lib.EINVAL
+    assert lib.olpe_moments_set(None, 0, None, None) == _lib.EINVAL
+    assert lib.olpe_moments_summary(None, None, None) == _lib.EINVAL
+    assert lib.olpe_comm_allreduce_moments(None, None) == _lib.EINVAL
+    assert lib.olpe_csv_shape(None, None, None) == _lib.EINVAL
+    assert lib.olpe_csv_read_chains(None, 1, 1, 1, 0, None, 0) == _lib.EINVAL
     lib.olpe_destroy(None)
+
+
+def test_empty_and_oversized_cutouts_are_rejected(lib):
+    """Shapes the reference cannot take either: an empty image, one wider than the
+    4096-pixel limit, an unknown dtype, a NULL image -- EINVAL before any GPU call."""
+    ctx = C.c_void_p()
+    img = np.zeros((8, 8), np.float32)
+    for ny, nx, dt, ptr in ((0, 0, 0, img.ctypes.data), (4097, 4097, 0, img.ctypes.data),
+                            (8, 8, 7, img.ctypes.data), (8, 8, 0, None)):
+        assert lib.olpe_create(ptr, dt, img.ctypes.data, 1444.0, None, ny, nx, 2, 0, 0,
+                               C.byref(ctx)) == _lib.EINVAL, (ny, nx, dt)
+    assert not ctx.value
 
 
 def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):
