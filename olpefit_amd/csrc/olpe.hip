@@ -1071,6 +1071,10 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
     }
     return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
   }
+  // large cutouts (a full 1024 x 1024 NIRC2 frame): one wave per workgroup once four
+  // waves' row tables (n x 2 NSRC doubles each) no longer fit the LDS; olpe_create
+  // rejects sides where even one does not
+  if (lds_bytes(c, 4) > 160 * 1024) return launch_gibbs_t<NSRC, 0, false, 1, FAST>(c, a);
   return launch_gibbs_t<NSRC, 0, false, 4, FAST>(c, a);
 }
 
@@ -1149,6 +1153,15 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
                    "(apf_step2.py:237, :119-123)", ny, nx);
   if (nx > 4096) return set_err(OLPE_EINVAL, "image too large (%d)", nx);
   if (nsrc != 2 && nsrc != 3) return set_err(OLPE_EINVAL, "nsrc must be 2 or 3");
+  {
+    // the largest sampler workgroup is one wave with its row tables (n x 2 nsrc doubles)
+    // and wave slice in the 160 KiB of LDS: sides up to 2,500 (2 sources) / 1,660 (3)
+    const size_t one = wave_lds(nx, nsrc == 2 ? 16 : 19, false) + kSampHdr;
+    if (one > 160 * 1024)
+      return set_err(OLPE_EINVAL, "%dx%d cutout: its row tables need %zu bytes of LDS per "
+                     "wave, more than the 163840 a workgroup has (cut the frame to the stars)",
+                     nx, nx, one);
+  }
   if (image_dtype != OLPE_DTYPE_F32 && image_dtype != OLPE_DTYPE_F64)
     return set_err(OLPE_EINVAL, "image_dtype must be OLPE_DTYPE_F32/F64");
   if (bkgd_mode != 0 && bkgd_mode != 1) return set_err(OLPE_EINVAL, "bkgd_mode must be 0/1");
@@ -1310,11 +1323,24 @@ static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, boo
   if (c->scratch2_cap < pout && (rc = dev_alloc(&c->d_scratch2, pout))) return rc;
   if (c->scratch2_cap < pout) c->scratch2_cap = pout;
   HIPCHK(hipMemcpyAsync(c->d_scratch, params, pin * 8, hipMemcpyHostToDevice, c->stream));
-  const int wpb = 4;
+  // four vectors per workgroup, fewer where their row tables would not fit the LDS
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * vtab_bytes(c->n, c->nsrc) + kEtabBytes > 160 * 1024) wpb /= 2;
   dim3 grid((W + wpb - 1) / wpb), block(wpb * 64);
   const size_t shm = (size_t)wpb * vtab_bytes(c->n, c->nsrc) + kEtabBytes;
   const int fast = c->eval_mode == OLPE_EVAL_FAST;
-  if (shm > 65536) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
+  if (shm > 160 * 1024) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
+  if (shm > 65536) {
+    static std::atomic<int> eval_attr{0};
+    if (!eval_attr.exchange(1)) {
+      const void *ks[4] = {(const void *)olpe_eval_kernel<2, true>,
+                           (const void *)olpe_eval_kernel<2, false>,
+                           (const void *)olpe_eval_kernel<3, true>,
+                           (const void *)olpe_eval_kernel<3, false>};
+      for (const void *k : ks)
+        HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
+  }
   if (c->nsrc == 2) {
     if (write)
       hipLaunchKernelGGL((olpe_eval_kernel<2, true>), grid, block, shm, c->stream, fast ? c->d_DW : c->d_DE,

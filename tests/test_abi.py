@@ -102,6 +102,10 @@ def test_empty_and_oversized_cutouts_are_rejected(lib):
         assert lib.olpe_create(ptr, dt, img.ctypes.data, 1444.0, None, ny, nx, 2, 0, 0,
                                C.byref(ctx)) == _lib.EINVAL, (ny, nx, dt)
     assert not ctx.value
+    # a side whose one-wave row tables exceed the LDS (3 sources, 48 B per row)
+    assert lib.olpe_create(img.ctypes.data, 0, img.ctypes.data, 1444.0, None, 4000, 4000, 3,
+                           0, 0, C.byref(ctx)) == _lib.EINVAL
+    assert b"LDS" in lib.olpe_last_error()
 
 
 def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):

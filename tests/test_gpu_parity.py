@@ -755,6 +755,36 @@ def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
 
 
+@pytest.mark.parametrize("n,nsrc,mode", [(1024, 2, "fast"), (900, 3, "exact"), (600, 2, "exact")])
+def test_full_frame_cutouts_match_oracle(lib_loaded, n, nsrc, mode):
+    """Frames far beyond the cutout sizes of the bench (a full 1024 x 1024 NIRC2 frame):
+    the row tables of four waves no longer fit the LDS, so the sampler runs one-wave
+    workgroups and the model / chi^2 kernel fewer vectors per workgroup; model, chi^2
+    and 2 walkers x 24 iterations against the oracle (the reference evaluates the whole
+    frame every proposal, apf_step2.py:94)."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    img, _ = synth.make_image(n, nsrc, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
+    with np.errstate(all="ignore"):
+        ref_model = ora.build_analytical_model(p0, n, nsrc)
+        p0[-1] = float(ora.chi_squared(dm, ref_model, err))
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode(mode)
+    m = s.build_analytical_model(p0)
+    assert np.max(np.abs(m - ref_model)) <= TOL[mode]["model"] * np.max(np.abs(ref_model))
+    assert abs(s.chi_squared(p0) - p0[-1]) <= TOL[mode]["chi"] * p0[-1]
+    seeds = [41, 42]
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (2, 1)))
+    chain = s.run(24, burn_in=0, record_stride=1)
+    for w, sd in enumerate(seeds):
+        ref, _ = ora.Walker(dm, err, p0, sd, nsrc=nsrc).run(24)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+
+
 @pytest.mark.parametrize("core", [(0.3, 0.3, 0.0), (0.3, 0.5, 0.7), (0.6, 0.45, -0.4)])
 @pytest.mark.parametrize("wpb", ["12", "16"])
 def test_sampler_fallback_sweeps_match_oracle(golden, lib_loaded, core, wpb, monkeypatch):
