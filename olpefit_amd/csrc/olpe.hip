@@ -1155,7 +1155,8 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   if (nsrc != 2 && nsrc != 3) return set_err(OLPE_EINVAL, "nsrc must be 2 or 3");
   {
     // the largest sampler workgroup is one wave with its row tables (n x 2 nsrc doubles)
-    // and wave slice in the 160 KiB of LDS: sides up to 2,500 (2 sources) / 1,660 (3)
+    // and wave slice in the 160 KiB of LDS: sides up to ~5,000 with 2 sources (the 4,096
+    // cap comes first) and ~3,380 with 3
     const size_t one = wave_lds(nx, nsrc == 2 ? 16 : 19, false) + kSampHdr;
     if (one > 160 * 1024)
       return set_err(OLPE_EINVAL, "%dx%d cutout: its row tables need %zu bytes of LDS per "
