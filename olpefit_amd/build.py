@@ -26,10 +26,40 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          "-Wall", "-Wno-unused-function"]
 
 
-def kernel_digest() -> str:
-    """16 hex digits over the device sources and flags: tags measured per-kernel
-    counts (profiles/valu_counts.json) with the code they were measured on."""
+def _elf_section(path: str, name: str) -> bytes:
+    """The bytes of one section of an ELF64 little-endian file (None if absent)."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    def sec(i):
+        return struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+    _, _, _, _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        nm, _, _, _, off, size = sec(i)
+        end = data.index(b"\0", stroff + nm)
+        if data[stroff + nm:end].decode() == name:
+            return data[off:off + size]
+    return None
+
+
+def kernel_digest(lib: str = LIB) -> str:
+    """16 hex digits identifying the sampler's device code: tags measured per-kernel
+    counts (profiles/valu_counts.json) with the code they were measured on.  It is the
+    hash of the built library's device code objects (its .hip_fatbin section: the same
+    bytes whenever the device code is the same -- an edit to host code, a comment or a
+    diagnostic build's hook leaves it unchanged); without a library, the hash of the
+    flags and the device sources' text."""
     import hashlib
+    try:
+        fat = _elf_section(lib, ".hip_fatbin")
+    except OSError:
+        fat = None
+    if fat:
+        return hashlib.sha256(b"fatbin:" + fat).hexdigest()[:16]
     h = hashlib.sha256(" ".join(FLAGS).encode())
     for f in ("olpe.hip", "olpe_device.h", "exp_table.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:

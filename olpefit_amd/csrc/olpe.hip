@@ -1116,6 +1116,14 @@ extern "C" {
 
 int olpe_version(void) { return 101; }
 
+#ifdef OLPE_DIAG_FALLBACK
+// diagnostic build only: the sweep-kind counters of olpe_device.h (tools/diag_fallback.py)
+int olpe_diag_fallback(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_fb), 4 * sizeof(unsigned long long)) ==
+                 hipSuccess ? OLPE_OK : OLPE_EHIP;
+}
+#endif
+
 const char *olpe_last_error(void) { return g_err; }
 
 int olpe_device_count(int *count) {

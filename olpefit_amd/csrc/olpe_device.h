@@ -237,6 +237,12 @@ __device__ __forceinline__ double accept_threshold(double u) {
 }
 constexpr int kThr = 129;       // MTWave::tab offset of the accept thresholds
 
+#ifdef OLPE_DIAG_FALLBACK
+// diagnostic build only (tools/diag_fallback.py): sampler sweeps by kind, [0] FAST3,
+// [1] FAST2, [2] V table, [3] exact
+__device__ unsigned long long g_diag_fb[4];
+#endif
+
 struct MTWave {
   uint32_t *key;  // HBM, MT_N words (this walker's row)
   int pos;        // numpy state->pos (uniform)
@@ -1960,6 +1966,9 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     }
 #endif
     asm volatile("" ::: "memory");
+#ifdef OLPE_DIAG_FALLBACK
+    if (!WRITE && lane == 0) atomicAdd(&g_diag_fb[ok3 ? 0 : (fast_level<NSRC>(m, nn) == 2 ? 1 : fast_level<NSRC>(m, nn) == 1 ? 2 : 3)], 1ull);
+#endif
     if (ok3) {
       const int tw = 2 * rows0;                            // doubles per slot
       const double *h;
