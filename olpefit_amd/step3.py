@@ -164,3 +164,81 @@ def pooled_mean(parts):
     parts = np.asarray(parts)
     ps = parts.shape[1] // 5
     return parts[:, 2:2 + ps].sum(axis=0) / parts[:, 1].sum()
+
+
+def main(argv=None, nsrc: int = 2):
+    """The step-3 command line up to the statistics this build covers: apf_step3.py's
+    arguments (positional ``image`` and ``system``, ``-s/--size`` walkers,
+    ``-a/--additional_burnin``, :64-84), its read of the chain files (:160-186, native
+    loader), its burn-in slice (:190-205) and its Gelman-Rubin statistics (:258-278),
+    printed as the reference prints them, then per-parameter mean / median / sigma and
+    the acceptance (``posterior_summary.json`` when step 2 wrote one), written to
+    ``<frame>_apf_results/step3_summary.json``.  The distortion, refraction and
+    separation / PA stages after :278 need the NIRC2 distortion tables the reference
+    does not ship and a network name resolver: out of scope.
+    ``--from-moments`` skips the chain files and uses step 2's device moments."""
+    import argparse
+    import json
+    import sys
+    from . import pipeline
+    ap = argparse.ArgumentParser(prog="apf_step3" + ("" if nsrc == 2 else "_3body"))
+    ap.add_argument("image", help="the path to the image under study", type=str)
+    ap.add_argument("system", help="name of the system (Simbad look-up: not used here)",
+                    type=str)
+    ap.add_argument("-s", "--size", help="Number of processes", type=str, required=True)
+    ap.add_argument("-a", "--additional_burnin", type=int,
+                    help="Additional burn in to apply to chains")
+    ap.add_argument("--from-moments", action="store_true",
+                    help="statistics from step 2's posterior_summary.json (device moments; "
+                         "additional_burnin 1) instead of the chain files")
+    ap.add_argument("--npy", action="store_true", help="read the {i}_chain.npy sidecars")
+    ap.add_argument("-q", "--quiet", action="store_true")
+    args = ap.parse_args(sys.argv[1:] if argv is None else argv)
+    say = (lambda *a: None) if args.quiet else print
+    ncor = int(np.int_(args.size))                                  # :76-77
+    additional_burnin = args.additional_burnin or 1                 # :81-84
+    _, _, input_directory = pipeline.image_paths(args.image)       # :138-143
+    names = NAMES_2 if nsrc == 2 else NAMES_3
+    if args.from_moments:
+        with open(input_directory + "posterior_summary.json") as f:
+            summ = json.load(f)
+        if summ.get("_walkers") != ncor:
+            raise ValueError(f"posterior_summary.json holds {summ.get('_walkers')} walkers, "
+                             f"-s gives {ncor}")
+        stats = {k: summ[k] for k in names[:-1]}
+        length = summ["_rows_per_walker"] + 1
+    else:
+        say('Importing parameter arrays...')                        # :167
+        chains = load_chains(input_directory, ncor, 0, source="npy" if args.npy else "csv")
+        length = chains.shape[0]
+        say('Parameter array shape:', length)                       # :172
+        chains = chains[additional_burnin:length]                   # :190-205
+        stats = summary(chains, nsrc)
+    N = length - additional_burnin
+    say("Number of total jumps per walker:", length)                # :202-204
+    say("Number of jumps after additional burn in:", N)
+    say("Number of total samples after burn-in: ", N * ncor)
+    rc = np.array([stats[k]["gr_rc"] for k in names[:-1]])
+    say('Mean and stdev Gelman-Rubin stat for parameter chains:', np.mean(rc), np.std(rc))
+    say('GR for positions:', *rc[:4])                               # :277-278
+    if not args.from_moments:
+        try:
+            with open(input_directory + "posterior_summary.json") as f:
+                moments = json.load(f)
+            for k in names[:-1]:
+                for key in ("acceptance", "tries", "accepts"):
+                    if key in moments.get(k, {}):
+                        stats[k][key] = moments[k][key]
+        except (OSError, ValueError):
+            pass
+    for k in names[:-1]:
+        s = stats[k]
+        say(f"{k:>9} mean {s['mean']:.10g} median {s.get('median', float('nan')):.10g} "
+            f"std {s['std']:.6g} GR {s['gr_rc']:.6f}")
+    out = {"walkers": ncor, "rows_per_walker": N, "additional_burnin": additional_burnin,
+           "source": "moments" if args.from_moments else ("npy" if args.npy else "csv"),
+           "gr_rc_mean": float(np.mean(rc)), "gr_rc_std": float(np.std(rc)),
+           "parameters": stats}
+    with open(input_directory + "step3_summary.json", "w") as f:
+        json.dump(out, f, indent=1)
+    return out

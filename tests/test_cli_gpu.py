@@ -171,6 +171,11 @@ def test_cli_three_source_feeds_step3(tmp_path):
         np.testing.assert_allclose(c[:, w, :], ref, rtol=1e-9)
     s = step3.summary(c, nsrc=3)
     assert list(s) == step3.NAMES_3[:-1]
+    # the step-3 front end (3body/apf_step3_3body.py's arguments) on the same files
+    cli = step3.main([path, "system", "-s", "3", "-q"], nsrc=3)["parameters"]
+    for name in s:
+        for key in ("mean", "median", "std"):
+            assert cli[name][key] == s[name][key]
     for name in s:
         assert s[name]["gr_rc"] == np.sqrt(s[name]["gr_psrf"]) or np.isnan(s[name]["gr_rc"])
     # the device-moment summary of the 20-column chains (posterior_summary.json)

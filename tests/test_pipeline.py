@@ -320,3 +320,43 @@ def test_summary_from_moments_equals_summary(golden, nsrc):
     comb = step3.combine_moments(parts, dev)
     np.testing.assert_allclose(comb[2:], _moments_vector(chains)[2:] * np.r_[
         np.ones(3 * chains.shape[2]), 2 * np.ones(2 * chains.shape[2] - 2)], rtol=1e-12)
+
+
+def test_step3_cli_reads_step2_output(tmp_path, golden, capsys):
+    """apf_step3.py's front end (arguments image, system, -s, -a; apf_step3.py:64-84): it
+    reads the step-2 files of <frame>_apf_results/ (native loader), slices the burn-in
+    and prints the reference's Gelman-Rubin lines (:258-278); the statistics equal
+    step3.summary of the same chains, from the CSV files, the .npy sidecars or step 2's
+    posterior_summary.json."""
+    import json
+    g = golden("gr")
+    chains = g["chains2"]                                   # [N, M, 17]
+    N, M, ps = chains.shape
+    image = str(tmp_path / "N2.20250127.00042.LDIF.fits")
+    outdir = pipeline.image_paths(image)[2]
+    os.makedirs(outdir)
+    paths = [outdir + f"{w}_finalarray_mpi.csv" for w in range(M)]
+    pipeline.write_chain_csvs(paths, chains.transpose(1, 0, 2), nan_row=True)
+    pipeline.append_npy_chains([outdir + f"{w}_chain.npy" for w in range(M)],
+                               chains.transpose(1, 0, 2), N, 0)
+    ref = step3.summary(chains[2:], nsrc=2)                 # -a 3: the NaN row + 2 rows
+    out = step3.main([image, "HIP 1234", "-s", str(M), "-a", "3"])
+    text = capsys.readouterr().out
+    assert "Mean and stdev Gelman-Rubin stat for parameter chains:" in text
+    assert "Number of jumps after additional burn in: %d" % (N + 1 - 3) in text
+    for k, r in ref.items():
+        for key in ("mean", "median", "std", "gr_rc"):
+            assert out["parameters"][k][key] == r[key], (k, key)
+    assert json.load(open(outdir + "step3_summary.json"))["rows_per_walker"] == N - 2
+    npy = step3.main([image, "x", "-s", str(M), "-a", "3", "--npy", "-q"])
+    assert npy["parameters"] == out["parameters"]
+    # --from-moments: step 2's device-moment summary (here from host moments)
+    m = _moments_vector(chains)
+    with open(outdir + "posterior_summary.json", "w") as f:
+        json.dump(step3.summary_from_moments(m, 2), f)
+    mom = step3.main([image, "x", "-s", str(M), "--from-moments", "-q"])
+    full = step3.summary(chains, nsrc=2)
+    for k, r in full.items():
+        np.testing.assert_allclose(mom["parameters"][k]["gr_rc"], r["gr_rc"], rtol=5e-12)
+    with pytest.raises(ValueError):
+        step3.main([image, "x", "-s", str(M + 1), "--from-moments", "-q"])
