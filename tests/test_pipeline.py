@@ -163,6 +163,34 @@ def test_headless_step1_guess(tmp_path):
     assert text.endswith("\n") and len(text.split()) == 6
 
 
+def test_headless_step1_three_body(tmp_path):
+    """3body/apf_step1_3body.py:165-197: 8x8 box image[y-4:y+4, x-4:x+4] around each
+    truncated click, integer argmax position, file "xca yca xcb ycb xcc ycc bkgdx bkgdy"."""
+    from olpefit_amd import step1
+    path = synth.write_case(str(tmp_path), 64, 3)
+    img, _ = fitsio.getdata_header(path)
+    p = synth.truth_params(64, 3)
+    clicks = [(p[0] + 1.6, p[1] - 0.8), (p[2] - 1.2, p[3] + 2.1), (p[4] + 0.3, p[5] + 0.9)]
+    argv = [str(tmp_path), "--star", str(clicks[0][0]), str(clicks[0][1])]
+    for c in clicks[1:]:
+        argv += ["--companion", str(c[0]), str(c[1])]
+    out = step1.main(argv + ["--sky", "5.9", "3.1"], three_body=True)
+    text = open(out[0]).read()
+    assert text.endswith("\n")
+    vals = text.split()
+    assert len(vals) == 8 and all(v.lstrip("-").isdigit() for v in vals)
+    for k, (x, y) in enumerate(clicks):
+        xm, ym = int(x), int(y)
+        box = img[ym - 4:ym + 4, xm - 4:xm + 4]
+        yc, xc = np.unravel_index(np.argmax(box), box.shape)
+        assert (int(vals[2 * k]), int(vals[2 * k + 1])) == (xm - 4 + xc, ym - 4 + yc)
+    assert vals[6:] == ["5", "3"]
+    g = pipeline.read_guess(out[0])
+    assert len(g) == 8
+    with pytest.raises(SystemExit):      # two companions (B, C) required
+        step1.main(argv[:7] + ["--sky", "5.9", "3.1"], three_body=True)
+
+
 def test_native_csv_formatter_equals_repr():
     """olpe_csv_format (host-only, no GPU) writes what csv.writer writes for float rows
     (repr of each value): edge values, random magnitudes over 10^+-30, integers, and
