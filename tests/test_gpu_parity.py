@@ -755,6 +755,39 @@ def test_other_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
         np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
 
 
+@pytest.mark.parametrize("n,nsrc,mode", [(4, 2, "fast"), (5, 3, "fast"), (8, 2, "exact"),
+                                         (17, 3, "fast"), (33, 2, "exact"), (65, 2, "fast"),
+                                         (127, 3, "fast"), (129, 2, "fast")])
+def test_ragged_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
+    """Ragged sides: tiny cutouts (4 px, where the saturation mask leaves one pixel, and
+    5 px: a few columns per row group, most lanes idle) and odd sides around the 32 / 64
+    / 128 kernels (row groups that do not divide 64, one column past a pass).  The truth
+    vector of the synthetic frame as the start (a step-1 guess needs a 10 x 10 sky box);
+    model, chi^2 and 3 walkers x 200 iterations against the oracle."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    img, truth = synth.make_image(n, nsrc, 1)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = np.append(truth, 0.0)
+    with np.errstate(all="ignore"):
+        ref_model = ora.build_analytical_model(p0, n, nsrc)
+        p0[-1] = float(ora.chi_squared(dm, ref_model, err))
+    assert np.isfinite(p0[-1])
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode(mode)
+    m = s.build_analytical_model(p0)
+    assert np.max(np.abs(m - ref_model)) <= TOL[mode]["model"] * np.max(np.abs(ref_model))
+    assert abs(s.chi_squared(p0) - p0[-1]) <= TOL[mode]["chi"] * p0[-1]
+    seeds = [51, 52, 53]
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (3, 1)))
+    chain = s.run(200, burn_in=0, record_stride=2)
+    for w, sd in enumerate(seeds):
+        ref, _ = ora.Walker(dm, err, p0, sd, nsrc=nsrc).run(200, record_stride=2)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+    s.close()
+
+
 @pytest.mark.parametrize("n,nsrc,mode", [(1024, 2, "fast"), (900, 3, "exact"), (600, 2, "exact")])
 def test_full_frame_cutouts_match_oracle(lib_loaded, n, nsrc, mode):
     """Frames far beyond the cutout sizes of the bench (a full 1024 x 1024 NIRC2 frame):
