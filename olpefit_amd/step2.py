@@ -251,23 +251,16 @@ class Output:
                                            np.zeros((sh.W, 0, sh.s.ps)), 0, npy_rows)
         self.npy_rows = npy_rows
 
-    def commit(self, acceptance=True):
-        """Append every shard's last launch and rewrite the acceptance files
-        (str(total_accept / total_tries), apf_step2.py:362-365; the reference writes
-        them only once count >= burn_in, :342)."""
+    def commit(self):
+        """Append every shard's last launch (and fold it into the device moments)."""
         def body(g):
             sh = self.shards[g]
             rows = sh.last.shape[1]
             if rows:
                 sh.s.moments_accumulate()        # async, on the device
-            _, tries, acc = sh.s.get_state()
-            if self.csv:
-                if rows:
-                    # one writer thread per shard for step 2a, where the files are shared
-                    self.sizes[g] = pipeline.append_chain_csvs(self._paths(g, 0), sh.last)
-                if acceptance:
-                    for k, p in enumerate(self._paths(g, 1)):
-                        pipeline.write_acceptance(p, acc[k], tries[k])
+            if self.csv and rows:
+                # one writer thread per shard for step 2a, where the files are shared
+                self.sizes[g] = pipeline.append_chain_csvs(self._paths(g, 0), sh.last)
             if self.npy and rows:
                 pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
                                            sh.last, rows, self.npy_rows)
@@ -279,6 +272,23 @@ class Output:
             rows[g] = body(g)
         _parallel(self.shards, run)
         self.npy_rows += rows[0]
+
+    def write_acceptance(self):
+        """Rewrite the acceptance files, str(total_accept / total_tries) per walker
+        (apf_step2.py:362-365, written once count >= burn_in, :342).  The reference
+        rewrites them with the chain every 10 iterations; here at each checkpoint and at
+        the end of the run (the count the chain files end at), so a resumed run and an
+        uninterrupted one leave the same files.  (Per launch, 65,536 walkers' files took
+        longer to format than the launch ran.)"""
+        if not self.csv:
+            return
+
+        def run(sh):
+            g = self.shards.index(sh)
+            _, tries, acc = sh.s.get_state()
+            for k, p in enumerate(self._paths(g, 1)):
+                pipeline.write_acceptance(p, acc[k], tries[k])
+        _parallel(self.shards, run)
 
     def all_sizes(self):
         return np.concatenate(self.sizes)
@@ -448,7 +458,7 @@ def main(argv=None, nsrc=2, variant="2"):
         # launch: one holds every walker's MT key (190 MB at 65,536 walkers).  Rank 0's
         # clock decides for every rank, so that all checkpoints hold the same count.
         nonlocal launches, last_ckpt
-        out.commit(acceptance=count >= burn)
+        out.commit()
         launches += 1
         now = time.monotonic()
         due = bool((args.checkpoint_every and launches % args.checkpoint_every == 0) or
@@ -456,6 +466,8 @@ def main(argv=None, nsrc=2, variant="2"):
         if group is not None:
             due = bool(group.broadcast(due))
         if due:
+            if count >= max(burn, 1):
+                out.write_acceptance()
             save_checkpoint(ckpt, shards, out, count, config)
             last_ckpt = time.monotonic()
 
@@ -472,6 +484,8 @@ def main(argv=None, nsrc=2, variant="2"):
             count += n
             commit()
             say("Loop count:", count)
+        if count >= max(burn, 1):
+            out.write_acceptance()        # the files' count: the last multiple of 10
         if args.iters > max(count, last):
             run(args.iters - max(count, last), record=False)
     else:
@@ -500,6 +514,8 @@ def main(argv=None, nsrc=2, variant="2"):
                 run(stop - count)
                 count = stop
                 commit()
+            if count >= max(burn, 1):
+                out.write_acceptance()
             say("Loop count:", count)
             break
     if variant == "2":
