@@ -159,7 +159,7 @@ __host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, in
 // draw tables there (its sweeps park nothing) and the two FAST3 shape-table slots (no
 // V-table fallback)
 template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
-  return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
+  return WaveSlice<NP>::OPE + kDrawTabBytes + (OLPE_RING_WINDOW ? 1 : 2) * n * 16;
 }
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
@@ -466,7 +466,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
-    hcache.single = single_h(NSRC, NT, WPB, FAST);
+    hcache.single = single_h(NSRC, NT, WPB, FAST) || (RING && OLPE_RING_WINDOW);
     GuardCache gcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);

@@ -1198,11 +1198,13 @@ struct HCache {
   int flip = 0;
   int single = 0;       // one slot (olpe.hip single_h): a shape proposal rebuilds its set
                         // in place, so the slot is current only if the proposal is taken
+  int stale = 0;        // single slot: sets (bit 0 wide, bit 1 narrow) the slot holds
+                        // for another state than the current one; rebuilt when next used
   __device__ __forceinline__ void after(bool accepted) {
     if (single) {
-      // flip = this step rebuilt the slot in place (FAST3 taken); otherwise the slot
-      // still holds the state before the step
-      if (grp) valid = flip ? (int)accepted : valid & (int)!accepted;
+      // flip = this step rebuilt its set in place (FAST3 taken): stale unless accepted;
+      // otherwise the slot still holds the state before the step: stale if accepted
+      if (grp && (flip ? !accepted : accepted)) stale |= grp == 1 ? 2 : 1;
       flip = 0;
       return;
     }
@@ -1625,21 +1627,24 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // issuing wave's next LDS reads (it cannot tell the ring slots apart), and its own
 // counted waits stay correct because vector memory operations retire in order.
 //
-// Windowed form (OLPE_RING_WINDOW, round 3): four slots of 16-row phases, the DMA of
-// phase g + 2 issued at the start of phase g, and no s_barrier per phase: a wave that
-// starts phase g first waits for its own DMAs and LDS reads (so it no longer reads phase
-// g - 1 and its DMA shares so far have landed), counts itself in with an LDS atomic
-// (arrive[g % 4]), and then waits only until every wave has started phase g - 1 --
-// which is when phase g's DMA (issued at g - 2) has landed everywhere and the slot of
-// phase g + 2 (phase g - 2's) is read by nobody.  The waves of a workgroup may so drift
-// one phase apart: the oldest wave of a SIMD runs into the next phase while the
-// younger ones finish, instead of idling at a barrier.
+// Windowed form (OLPE_RING_WINDOW, round 3): five slots of 16-row phases, the DMA of
+// phase g + 3 issued at the start of phase g, and no s_barrier per phase: a wave that
+// starts phase g first waits for its LDS reads and for its DMA shares but the latest
+// phase's (so it no longer reads phase g - 1 and its share of phase g + 1 has landed),
+// counts itself in with an LDS atomic (arrive[g % 5]), and then waits only until every
+// wave has started phase g - 1 -- which is when phase g's DMA has landed everywhere and
+// the slot of phase g + 3 (phase g - 2's) is read by nobody.  The waves of a workgroup
+// may so drift one phase apart (the oldest wave of a SIMD runs into the next phase while
+// the younger ones finish, instead of idling at a barrier), and each DMA has two phases
+// to land.  (The first form, four slots with the DMA two phases ahead and every DMA
+// drained at the next phase, stalled on its own loads: 6 % slower.)  Its 80 KiB of ring
+// fit beside 12 wave slices with one shape-table slot per wave (HCache::single).
 #ifndef OLPE_RING_WINDOW
 #define OLPE_RING_WINDOW 0
 #endif
 template <int WAVES> struct LdsRing {
 #if OLPE_RING_WINDOW
-  static constexpr int ROWS = 16, SLOTS = 4, AHEAD = 2;
+  static constexpr int ROWS = 16, SLOTS = 5, AHEAD = 3;
 #else
   static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
   static constexpr int SLOTS = 2, AHEAD = 1;              // ring slots; DMA lead in phases
@@ -1658,6 +1663,7 @@ template <int WAVES> struct LdsRing {
   unsigned voff;         // lane * 16
 #if OLPE_RING_WINDOW
   unsigned *arrive;      // windowed form: [SLOTS] arrival counters after the slots
+  int nshare;            // DMA instructions of this wave per phase (its rows of the phase)
 #endif
 #ifdef OLPE_DIAG_TIMING
   // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
@@ -1700,6 +1706,7 @@ template <int WAVES> struct LdsRing {
     g = 0;
 #if OLPE_RING_WINDOW
     arrive = reinterpret_cast<unsigned *>(ring_lds + SLOTS * SLOT);
+    nshare = w < ROWS ? (ROWS - 1 - w) / WAVES + 1 : 0;
     if (w == 0 && lane < SLOTS) arrive[lane] = 0u;
 #pragma unroll
     for (int p = 0; p < AHEAD; ++p) dma_phase(p, p % SLOTS);
@@ -1714,7 +1721,18 @@ template <int WAVES> struct LdsRing {
 #ifdef OLPE_DIAG_TIMING
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // this wave's LDS reads done, and its DMA shares landed up to phase g + AHEAD - 2:
+    // only the latest phase's (issued at the previous begin_phase) may stay in flight, so
+    // the arrival below certifies this wave's share of phase g + 1 -- two phases after
+    // it was issued.  Vector memory operations retire in order.  At a step's first phase
+    // the step's control section (key loads, chain stores) sits after the latest DMA, so
+    // the wait there is for everything (more than needed, never less).
+    if (g % PHASES == 0 || g < (unsigned)AHEAD || nshare <= 0 || nshare > 2)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if (nshare == 1)
+      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
     typedef __attribute__((address_space(3))) unsigned lds_u32;
     lds_u32 *cnt = (lds_u32 *)arrive;
     if (voff == 0) __hip_atomic_fetch_add(cnt + g % SLOTS, 1u, __ATOMIC_RELAXED,
@@ -1975,19 +1993,23 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       if (!hc) {
         build_htab<NSRC>(m, vtab, vtab, 3, rows0, kc, (double)cw.S, lane, ExpTab{etab});
         h = vtab;
+      } else if (hc->single) {
+        // in place: this step's set (the proposal's) and the sets left stale by earlier
+        // steps (a rejected proposal's, or the state's before an accepted step that took
+        // another sweep); the other set stays
+        const int need = (hc->valid ? hc->stale : 3) | (hc->grp ? (hc->grp == 1 ? 2 : 1) : 0);
+        if (need)
+          build_htab<NSRC>(m, vtab, vtab, need, rows0, kc, (double)cw.S, lane, ExpTab{etab});
+        hc->valid = 1;
+        hc->stale = 0;
+        hc->flip = hc->grp != 0;
+        h = vtab;
       } else if (hc->grp == 0) {
         if (!hc->valid) {
           build_htab<NSRC>(m, vtab + hc->cur * tw, vtab, 3, rows0, kc, (double)cw.S, lane, ExpTab{etab});
           hc->valid = true;
         }
         h = vtab + hc->cur * tw;
-      } else if (hc->single) {
-        // in place: the proposal's set over the current state's (the other set copied
-        // onto itself); after a reject the slot is marked stale (HCache::after)
-        build_htab<NSRC>(m, vtab, vtab, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3, rows0, kc,
-                         (double)cw.S, lane, ExpTab{etab});
-        hc->flip = true;
-        h = vtab;
       } else {
         double *dst = vtab + (hc->cur ^ 1) * tw;
         build_htab<NSRC>(m, dst, vtab + hc->cur * tw, hc->valid ? (hc->grp == 1 ? 2 : 1) : 3,
