@@ -729,7 +729,8 @@ __device__ __forceinline__ double sweep_exact_rows(const ModelDesc<NSRC> &m, con
       t2[g] = m.g[g].k.b * xd;
     }
     // (two rows per trip; one for the 3-source 32x32 sampler, which spills with two)
-#pragma unroll(NSRC == 3 && NT == 32 ? 1 : 2)
+    constexpr int kRowUnroll = NSRC == 3 && NT == 32 ? 1 : 2;
+#pragma unroll kRowUnroll
     for (int i = grp; i < NT; i += S) {
       double v[G];
 #pragma unroll
