@@ -1014,7 +1014,9 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   {
     const double chunk = (double)((a.n_iters + q.units - 1) / q.units);
     const double ticks = chunk * (double)a.n * (double)a.n * (2.0 * NSRC) * 0.8;
-    q.wait_ticks = (unsigned long long)std::min(std::max(ticks, 3e9), 1e15);
+    q.wait_ticks = c->wait_ticks_override > 0
+                       ? (unsigned long long)c->wait_ticks_override
+                       : (unsigned long long)std::min(std::max(ticks, 3e9), 1e15);
     c->wait_limit_s = (double)q.wait_ticks * 1e-8;
   }
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
@@ -1283,6 +1285,8 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     c->ring_wpb = v;
   }
   if (const char *e = getenv("OLPE_STAGGER")) c->stagger = std::max(0, std::min(1000, atoi(e)));
+  // tests only: the hand-off wait limit in 100 MHz ticks instead of the launch's bound
+  if (const char *e = getenv("OLPE_WAIT_TICKS")) c->wait_ticks_override = std::max(0.0, atof(e));
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);
   if (e2 == hipSuccess)
     e2 = hipMemcpy(c->d_DW, hDW.data(), npix * sizeof(double2), hipMemcpyHostToDevice);

@@ -57,6 +57,7 @@ struct olpe_ctx {
   int last_units = 1;       // chunks per walker of the last launch (olpe_last_units)
   bool units_used = false;  // some launch handed chunks between waves (check_units)
   double wait_limit_s = 30; // hand-off wait limit of the last launch (unit_wait)
+  double wait_ticks_override = 0;  // OLPE_WAIT_TICKS (tests of the time-out path)
   int balance = -1;         // progress balancing (OLPE_BALANCE 0/1; -1: launch_gibbs_t picks)
   int ring_wpb = 12;        // 128x128 FAST: the lockstep LDS-ring sampler's waves per
                             // workgroup, 0 = the L2-resident sampler (OLPE_RING)

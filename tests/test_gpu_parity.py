@@ -605,6 +605,39 @@ def test_work_units_few_walkers_spin(golden, lib_loaded, monkeypatch, mode):
     assert got[5] == [15, 15, 15]
 
 
+def test_work_unit_handoff_timeout_is_reported(golden, lib_loaded, monkeypatch):
+    """The hand-off wait's time-out path (unit_wait): with the limit forced down to one
+    100 MHz tick (OLPE_WAIT_TICKS, a test hook), the waves of 13 walkers cut into 15
+    chunks give up on their predecessors and the launch reports the time-out instead of
+    returning results; the same launch under the launch's own bound (chunk-scaled, never
+    below 30 s) completes with the whole-walker results."""
+    g = golden("c32")
+    W = 13
+    seeds = 600 + np.arange(W)
+    monkeypatch.setenv("OLPE_NO_QUEUE", "0")
+    monkeypatch.setenv("OLPE_UNITS", "15")
+    monkeypatch.setenv("OLPE_WAIT_TICKS", "1")
+    s = make_sampler(g, "fast")
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    with pytest.raises(Exception, match="hand-off timed out"):
+        s.run(150, burn_in=0, record_stride=10)
+    s.close()
+    monkeypatch.delenv("OLPE_WAIT_TICKS")
+    s = make_sampler(g, "fast")
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    chain = s.run(150, burn_in=0, record_stride=10)
+    assert s.last_units() == 15 and s.unit_stats()[0] > 0
+    s.close()
+    monkeypatch.setenv("OLPE_UNITS", "1")
+    s = make_sampler(g, "fast")
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    np.testing.assert_array_equal(s.run(150, burn_in=0, record_stride=10), chain)
+    s.close()
+
+
 def test_work_units_l2_sampler(lib_loaded, monkeypatch):
     """The 128x128 (L2-resident) sampler runs persistent only when it cuts walkers
     into chunks: chunks of 3 and of 5 equal its static mapping bit for bit."""
