@@ -116,6 +116,8 @@ def parse(argv, nsrc, variant="2"):
                          "of LOCAL_RANK's GPUs (a rehearsal on a one-GPU host)")
     ap.add_argument("--no-csv", action="store_true")
     ap.add_argument("--npy", action="store_true", help="also write {w}_chain.npy")
+    ap.add_argument("--timing", action="store_true",
+                    help="print where the wall time went (launches, files, checkpoints)")
     ap.add_argument("-q", "--quiet", action="store_true")
     args = ap.parse_args(argv)
     args.mpi_rank, args.mpi_size = mpi_world() if variant == "2" else (0, 1)
@@ -175,6 +177,34 @@ def _parallel(shards, fn):
         t.join()
     if errs:
         raise errs[0]
+
+
+class _Background:
+    """One host job at a time beside the GPU work: the previous launch's chain-file
+    appends (and a checkpoint's acceptance files) while the next launch runs.  wait()
+    joins it and re-raises its error."""
+
+    def __init__(self):
+        self.t, self.err = None, None
+
+    def start(self, fn):
+        self.wait()
+
+        def body():
+            try:
+                fn()
+            except BaseException as e:      # re-raised by wait()
+                self.err = e
+        self.t = threading.Thread(target=body, daemon=True)
+        self.t.start()
+
+    def wait(self):
+        if self.t is not None:
+            self.t.join()
+            self.t = None
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise e
 
 
 def device_free_bytes(device: int) -> int:
@@ -251,19 +281,25 @@ class Output:
                                            np.zeros((sh.W, 0, sh.s.ps)), 0, npy_rows)
         self.npy_rows = npy_rows
 
-    def commit(self):
-        """Append every shard's last launch (and fold it into the device moments)."""
+    def fold(self):
+        """Fold every shard's last launch into its device moments (queued on the device
+        before the next launch, which overwrites the rows)."""
+        for sh in self.shards:
+            if sh.last.shape[1]:
+                sh.s.moments_accumulate()
+
+    def append(self, lasts):
+        """Append a launch's rows (lasts[g]: shard g's [W][rows][PS]) to the chain files;
+        host-only, so it may run beside the next launch."""
         def body(g):
-            sh = self.shards[g]
-            rows = sh.last.shape[1]
-            if rows:
-                sh.s.moments_accumulate()        # async, on the device
+            last = lasts[g]
+            rows = last.shape[1]
             if self.csv and rows:
                 # one writer thread per shard for step 2a, where the files are shared
-                self.sizes[g] = pipeline.append_chain_csvs(self._paths(g, 0), sh.last)
+                self.sizes[g] = pipeline.append_chain_csvs(self._paths(g, 0), last)
             if self.npy and rows:
                 pipeline.append_npy_chains([self.outdir + n for n in self.npy_names[g]],
-                                           sh.last, rows, self.npy_rows)
+                                           last, rows, self.npy_rows)
             return rows
         rows = [0] * len(self.shards)
 
@@ -273,19 +309,30 @@ class Output:
         _parallel(self.shards, run)
         self.npy_rows += rows[0]
 
-    def write_acceptance(self):
+    def commit(self):
+        """Append every shard's last launch and fold it into the device moments."""
+        self.fold()
+        self.append([sh.last for sh in self.shards])
+
+    def acceptance_counts(self):
+        """Every shard's (tries, accepts) now, for write_acceptance."""
+        return [sh.s.get_state()[1:] for sh in self.shards]
+
+    def write_acceptance(self, counts=None):
         """Rewrite the acceptance files, str(total_accept / total_tries) per walker
         (apf_step2.py:362-365, written once count >= burn_in, :342).  The reference
         rewrites them with the chain every 10 iterations; here at each checkpoint and at
         the end of the run (the count the chain files end at), so a resumed run and an
         uninterrupted one leave the same files.  (Per launch, 65,536 walkers' files took
-        longer to format than the launch ran.)"""
+        longer to format than the launch ran.)  counts: acceptance_counts() taken earlier
+        (host-only then, so it may run beside the next launch)."""
         if not self.csv:
             return
+        counts = counts if counts is not None else self.acceptance_counts()
 
         def run(sh):
             g = self.shards.index(sh)
-            _, tries, acc = sh.s.get_state()
+            tries, acc = counts[g]
             for k, p in enumerate(self._paths(g, 1)):
                 pipeline.write_acceptance(p, acc[k], tries[k])
         _parallel(self.shards, run)
@@ -452,13 +499,38 @@ def main(argv=None, nsrc=2, variant="2"):
         chunk = int(-group.allmax(-chunk))
     launches = 0
     last_ckpt = time.monotonic()
+    tm = {}                                 # --timing: seconds per kind of work
+
+    class timed:
+        def __init__(self, key):
+            self.key = key
+
+        def __enter__(self):
+            self.t0 = time.perf_counter()
+
+        def __exit__(self, *exc):
+            tm[self.key] = tm.get(self.key, 0.0) + time.perf_counter() - self.t0
+
+    t_loop = time.perf_counter()
+
+    bg = _Background()
+
+    def settle():
+        with timed("waiting for the file writer"):
+            bg.wait()
 
     def commit():
-        # checkpoints are spaced by time (and optionally by launches), not written per
+        # the launch's rows are folded into the device moments now (queued before the
+        # next launch) and appended to the files beside the next launch (bg).
+        # Checkpoints are spaced by time (and optionally by launches), not written per
         # launch: one holds every walker's MT key (190 MB at 65,536 walkers).  Rank 0's
         # clock decides for every rank, so that all checkpoints hold the same count.
         nonlocal launches, last_ckpt
-        out.commit()
+        with timed("moment fold"):
+            out.fold()
+        lasts = [sh.last for sh in shards]
+        settle()                          # the files take the launches in order
+        bg.start(lambda: out.append(lasts))
         launches += 1
         now = time.monotonic()
         due = bool((args.checkpoint_every and launches % args.checkpoint_every == 0) or
@@ -466,13 +538,23 @@ def main(argv=None, nsrc=2, variant="2"):
         if group is not None:
             due = bool(group.broadcast(due))
         if due:
-            if count >= max(burn, 1):
-                out.write_acceptance()
-            save_checkpoint(ckpt, shards, out, count, config)
+            settle()                      # the recorded file sizes
+            counts = out.acceptance_counts() if count >= max(burn, 1) else None
+            with timed("checkpoints"):
+                save_checkpoint(ckpt, shards, out, count, config)
+            if counts is not None:        # the checkpoint's count, beside the next launch
+                bg.start(lambda: out.write_acceptance(counts))
             last_ckpt = time.monotonic()
 
+    def final_acceptance():
+        settle()
+        if count >= max(burn, 1):
+            with timed("acceptance files"):
+                out.write_acceptance()
+
     def run(n, accept_min=0, record=True):
-        _parallel(shards, lambda sh: sh.run(n, burn, stride if record else 0, accept_min))
+        with timed("launches (sampler + chain copy)"):
+            _parallel(shards, lambda sh: sh.run(n, burn, stride if record else 0, accept_min))
 
     if args.iters:
         # the files hold rows up to L = the last multiple of 10 <= iters (:355); the
@@ -484,8 +566,7 @@ def main(argv=None, nsrc=2, variant="2"):
             count += n
             commit()
             say("Loop count:", count)
-        if count >= max(burn, 1):
-            out.write_acceptance()        # the files' count: the last multiple of 10
+        final_acceptance()                # the files' count: the last multiple of 10
         if args.iters > max(count, last):
             run(args.iters - max(count, last), record=False)
     else:
@@ -494,11 +575,22 @@ def main(argv=None, nsrc=2, variant="2"):
         # every file then holds rows up to L = the last multiple of 10 <= C (:355).
         # Launches start at multiples of 10, so L lies inside the launch that found C:
         # that launch is re-run from its snapshot (RNG included, hence identical) up to L.
+        # Every walker's tries sum to the count, so min(tries) <= count / NP: no walker can
+        # reach accept_min before count = NP * accept_min, and only the launches from
+        # there on need the snapshot for the re-run (the MT keys, 2.5 KB per walker: 164 MB
+        # per launch at 65,536 walkers)
+        n_par = shards[0].s.ps - 1
         while True:
-            snaps = [sh.snapshot() for sh in shards]
+            need = args.accept_min <= 0 or count + chunk >= n_par * args.accept_min
+            with timed("snapshots"):
+                snaps = [sh.snapshot() for sh in shards] if need else None
             run(chunk, args.accept_min)
-            hits = np.concatenate([sh.s.done_at() for sh in shards])
+            with timed("launches (sampler + chain copy)"):
+                hits = np.concatenate([sh.s.done_at() for sh in shards])
             hits = hits[hits >= 0]
+            if hits.size and snaps is None:
+                raise RuntimeError(f"accept_min reached at count {int(hits.min())} before "
+                                   f"{n_par} x {args.accept_min} iterations")
             if group is not None:         # the earliest hit over every rank's walkers
                 first = group.allmax(-float(hits.min()) if hits.size else -np.inf)
                 hits = np.array([int(-first)]) if np.isfinite(first) else hits[:0]
@@ -514,10 +606,10 @@ def main(argv=None, nsrc=2, variant="2"):
                 run(stop - count)
                 count = stop
                 commit()
-            if count >= max(burn, 1):
-                out.write_acceptance()
+            final_acceptance()
             say("Loop count:", count)
             break
+    t_summ = time.perf_counter()
     if variant == "2":
         summ = posterior_summary(shards, nsrc, group)
         if rank == 0:
@@ -526,6 +618,13 @@ def main(argv=None, nsrc=2, variant="2"):
         if summ["_rows_per_walker"] > 1:
             say("Posterior (device moments):", {k: round(summ[k]["mean"], 6)
                                                 for k in list(summ)[:4]})
+    tm["posterior summary"] = time.perf_counter() - t_summ
+    if args.timing and rank == 0:
+        total = time.perf_counter() - t_loop
+        print(f"timing ({launches} launches of {chunk} iterations, {total:.2f} s):")
+        for k, v in sorted(tm.items(), key=lambda kv: -kv[1]):
+            print(f"  {k:32s} {v:8.2f} s")
+        print(f"  {'other':32s} {total - sum(tm.values()):8.2f} s")
     if os.path.exists(ckpt):
         os.remove(ckpt)                  # the run is complete: nothing to resume
     for sh in shards:

@@ -13,7 +13,7 @@ trap 'rm -rf "$D"' EXIT
 P=$(python -c "import sys; sys.path.insert(0, '.'); from olpefit_amd import synth; print(synth.write_case('$D', $N, $NS))")
 OUT=$(dirname "$P")/$(basename "$P" | cut -d. -f3)_apf_results
 t0=$(date +%s.%N)
-python $S2 "$P" --walkers $W --record-stride $ST --seed 1 -q
+python -u $S2 "$P" --walkers $W --record-stride $ST --seed 1 --timing | grep --line-buffered -v "^Initial guess"   # progress lines: a long run is not silent
 t1=$(date +%s.%N)
 python - "$OUT" "$W" "$t0" "$t1" "$N" "$NS" <<'PY'
 import json, os, sys
