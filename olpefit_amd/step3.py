@@ -74,13 +74,14 @@ def gelman_rubin(p, d: int = 16):
     that floor division here; a float ``d`` divides as floats, as it would there."""
     p = np.asarray(p, dtype=np.float64)
     N, M = float(p.shape[0]), float(p.shape[1])
-    ncor = p.shape[1]
-    w, b = np.zeros(ncor), np.zeros(ncor)
     overall_mean = np.mean(p)
-    for i in range(ncor):                        # per column, as the reference does
-        chain_mean = np.mean(p[:, i])
-        w[i] = np.std(p[:, i]) ** 2
-        b[i] = (chain_mean - overall_mean) ** 2
+    # the reference's per-column loop (np.mean / np.std of p[:, i]) as row reductions of
+    # the transpose: the same pairwise sums over the same values, so the same bits
+    # (a Python loop over 65,536 walkers took 45 s of step 3)
+    pt = np.ascontiguousarray(p.T)
+    chain_mean = np.mean(pt, axis=1)
+    w = np.std(pt, axis=1) ** 2
+    b = (chain_mean - overall_mean) ** 2
     w = (1. / M) * np.sum(w)
     b = (N / (M - 1)) * np.sum(b)
     pooled = ((N - 1) / N) * w + ((M + 1) / (M * N)) * b
