@@ -102,6 +102,32 @@ def test_noise_model_matches_oracle(golden):
     assert np.array_equal(err, g["err"])
 
 
+def test_gelman_rubin_equals_the_per_walker_loop():
+    """step3.gelman_rubin reduces the transposed chains row by row; apf_step3.py:260-276
+    loops over the walkers (np.mean / np.std of each column).  Same pairwise sums over
+    the same values: the same bits, C- or Fortran-ordered input, odd shapes."""
+    from olpefit_amd import step3
+
+    def loop(p, d=16):
+        N, M = float(p.shape[0]), float(p.shape[1])
+        w, b = np.zeros(p.shape[1]), np.zeros(p.shape[1])
+        om = np.mean(p)
+        for i in range(p.shape[1]):
+            w[i] = np.std(p[:, i]) ** 2
+            b[i] = (np.mean(p[:, i]) - om) ** 2
+        w = (1. / M) * np.sum(w)
+        b = (N / (M - 1)) * np.sum(b)
+        psrf = (((N - 1) / N) * w + ((M + 1) / (M * N)) * b) / w
+        return psrf, np.sqrt(((d + 3) // (d + 1)) * psrf)
+    rng = np.random.default_rng(11)
+    for t in range(60):
+        p = rng.normal(size=(int(rng.integers(2, 300)), int(rng.integers(2, 200))))
+        p = p * rng.uniform(1e-3, 1e3) + rng.uniform(-1e4, 1e4)
+        if t % 2:
+            p = np.asfortranarray(p)
+        assert step3.gelman_rubin(p) == loop(p)
+
+
 def test_step3_reader_and_gelman_rubin(tmp_path, golden):
     """Write chains with the build's writer, read them back with the step-3 contract
     (equal lengths, NaN row dropped by additional_burnin=1) and compare GR with the
