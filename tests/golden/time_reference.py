@@ -1,21 +1,23 @@
 """Time the reference's own apf_step2 loop against the oracle's NumPy restatement, one
 core, on the same frame (this container: the reference cannot travel to the GPU box).
 
-    /opt/conda/bin/python3.9 tools/time_reference.py [n] [nsrc] [accept_min]
+    /opt/conda/bin/python3.9 tests/golden/time_reference.py [n] [nsrc] [accept_min]
 
 Runs apf_step2.py's loop lines (:298-338, or 3body :324-373) through the fixture
 harness of tests/golden/make_golden.py (the reference's own function definitions and
 setup, astropy 4.3.1 models, a stand-in comm) with burn_in past the run, so no chain
 rows are stacked or written -- the sampling alone -- and then oracle/olpe_oracle.py's
 Walker over the same number of iterations.  Prints iterations per second of each.
+(Test infrastructure, like bench.py's cpu_baseline leg: the oracle is timed as the CPU
+baseline, never as the product.)
 """
 import os
 import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REPO = os.path.dirname(HERE)
-sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
 sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
