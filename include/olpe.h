@@ -190,6 +190,18 @@ int olpe_csv_shape(const char *path, long long *rows, int *cols);
 int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, int ncols,
                          long long skip, double *out, int threads);
 
+/* Step 2's acceptance files (apf_step2.py:362-365: str(total_accept / total_tries), NumPy's
+ * print of a float64 array).  Host-only.  olpe_acceptance_write: file i gets
+ * accepts[i][np] / tries[i][np] as NumPy prints it, from `threads` threads (0 = one per
+ * core), for the rows NumPy prints in fixed notation (all values finite, the non-zero
+ * ones in [1e-4, 1e8) within a factor 1000 of each other): done[i] = 1; done[i] = 0 for
+ * the rows left to the caller (scientific notation, NaN).  olpe_acceptance_format: the
+ * text for x[0..n) (*len_out = 0 when x is outside that range; out may be NULL to query
+ * the size). */
+int olpe_acceptance_format(const double *x, int n, char *out, size_t cap, size_t *len_out);
+int olpe_acceptance_write(const char *const *paths, const double *accepts, const double *tries,
+                          int nfiles, int np, int threads, unsigned char *done);
+
 /* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
 int olpe_comm_unique_id(uint8_t *id128);

@@ -68,6 +68,8 @@ SIGNATURES = {
     "olpe_csv_append_chains": (_i, [C.POINTER(C.c_char_p), _pd, _i, _ll, _ll, _i, _i, _pll]),
     "olpe_csv_shape": (_i, [C.c_char_p, _pll, C.POINTER(_i)]),
     "olpe_csv_read_chains": (_i, [C.POINTER(C.c_char_p), _i, _ll, _i, _ll, _pd, _i]),
+    "olpe_acceptance_format": (_i, [_pd, _i, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "olpe_acceptance_write": (_i, [C.POINTER(C.c_char_p), _pd, _pd, _i, _i, _i, _pu8]),
     "olpe_moments_accumulate": (_i, [_P]),
     "olpe_moments_reset": (_i, [_P]),
     "olpe_moments_get": (_i, [_P, _pll, _pd, _pd]),

@@ -17,6 +17,7 @@
 // arrays): it parses every file from a pool of threads straight into that layout.
 // std::from_chars rounds correctly, as Python's float() does, so the values are the
 // ones genfromtxt returns, bit for bit.
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -361,6 +362,143 @@ int olpe_csv_read_chains(const char *const *paths, int nfiles, long long nrows, 
     if (failed[t] >= 0)
       return olpe::set_err(why[t] == "cannot read" ? OLPE_EIO : OLPE_EINVAL,
                            "olpe_csv_read_chains: %s: %s", paths[failed[t]], why[t].c_str());
+  return OLPE_OK;
+}
+
+}  // extern "C"
+
+// --- acceptance files (apf_step2.py:362-365) -----------------------------------------
+// The reference writes str(total_accept / total_tries): NumPy's print of a float64
+// array.  For the arrays an accept / tries ratio gives -- every value finite, the
+// non-zero ones in [1e-4, 1e8) and within a factor 1000 of each other -- NumPy prints
+// in fixed notation ('maxprec', precision 8): each value's shortest round-trip digits,
+// cut to 8 fractional digits (correctly rounded, trailing zeros dropped) when they are
+// longer, the integer parts right-aligned and the fractions left-aligned to the widest,
+// ' ' between values, '[' ... ']' and lines wrapped at 75 characters with a one-space
+// indent (numpy/_core/arrayprint.py: FloatingFormat, _formatArray, _extendLine).  Other
+// arrays (scientific notation, NaN from a never-tried parameter) are left to the caller.
+namespace {
+
+// digits of v >= 0 as NumPy's dragon4_positional(v, precision=8, unique=True,
+// fractional=True, trim='.'): integer part and fraction (without the point)
+void positional8(double v, std::string &ip, std::string &fp) {
+  char buf[64];
+  std::to_chars_result r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::fixed);
+  std::string s(buf, r.ptr);
+  size_t dot = s.find('.');
+  if (dot != std::string::npos && s.size() - dot - 1 > 8) {
+    r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::fixed, 8);
+    s.assign(buf, r.ptr);
+    dot = s.find('.');
+    while (!s.empty() && s.back() == '0') s.pop_back();
+  }
+  if (dot == std::string::npos) {
+    ip = s;
+    fp.clear();
+  } else {
+    ip = s.substr(0, dot);
+    fp = s.substr(dot + 1);
+  }
+}
+
+// str(np.array(x)) for x[0..n) in the fixed-notation range; false otherwise
+bool numpy_str_fixed(const double *x, int n, std::string &out) {
+  double mx = 0.0, mn = 0.0;
+  bool any = false;
+  for (int i = 0; i < n; ++i) {
+    if (!std::isfinite(x[i]) || x[i] < 0.0 || std::signbit(x[i])) return false;
+    if (x[i] != 0.0) {
+      mx = any ? std::max(mx, x[i]) : x[i];
+      mn = any ? std::min(mn, x[i]) : x[i];
+      any = true;
+    }
+  }
+  if (any && (mx >= 1.e8 || mn < 0.0001 || mx / mn > 1000.)) return false;
+  std::vector<std::string> ip(n), fp(n);
+  size_t pl = 0, pr = 0;
+  for (int i = 0; i < n; ++i) {
+    positional8(x[i], ip[i], fp[i]);
+    pl = std::max(pl, ip[i].size());
+    pr = std::max(pr, fp[i].size());
+  }
+  // _formatArray, one axis: line width 75 - len(']'), hanging indent ' '
+  const size_t width = 74;
+  std::string s, line = " ";
+  for (int i = 0; i < n; ++i) {
+    std::string word(pl - ip[i].size(), ' ');
+    word += ip[i];
+    word += '.';
+    word += fp[i];
+    word.append(pr - fp[i].size(), ' ');
+    if (line.size() + word.size() > width && line.size() > 1) {
+      size_t e = line.find_last_not_of(' ');
+      s.append(line, 0, e == std::string::npos ? 0 : e + 1);
+      s += '\n';
+      line = " ";
+    }
+    line += word;
+    if (i + 1 < n) line += ' ';
+  }
+  s += line;
+  out = "[" + s.substr(1) + "]";
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int olpe_acceptance_format(const double *x, int n, char *out, size_t cap, size_t *len_out) {
+  if (!x || n <= 0 || !len_out) return olpe::set_err(OLPE_EINVAL, "olpe_acceptance_format: bad arguments");
+  std::string s;
+  if (!numpy_str_fixed(x, n, s)) {
+    *len_out = 0;
+    return OLPE_OK;
+  }
+  *len_out = s.size();
+  if (out) {
+    if (cap < s.size()) return olpe::set_err(OLPE_EINVAL, "olpe_acceptance_format: %zu bytes needed", s.size());
+    memcpy(out, s.data(), s.size());
+  }
+  return OLPE_OK;
+}
+
+int olpe_acceptance_write(const char *const *paths, const double *accepts, const double *tries,
+                          int nfiles, int np, int threads, unsigned char *done) {
+  if (!paths || !accepts || !tries || !done || nfiles < 0 || np <= 0)
+    return olpe::set_err(OLPE_EINVAL, "olpe_acceptance_write: bad arguments");
+  unsigned nt = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
+  if (nt == 0) nt = 1;
+  if (nt > 64) nt = 64;
+  if (nt > (unsigned)nfiles) nt = (unsigned)(nfiles > 0 ? nfiles : 1);
+  std::vector<int> failed(nt, -1);
+  auto work = [&](unsigned t) {
+    std::vector<double> x(np);
+    std::string s;
+    for (int i = (int)t; i < nfiles; i += (int)nt) {
+      for (int k = 0; k < np; ++k) x[k] = accepts[(size_t)i * np + k] / tries[(size_t)i * np + k];
+      done[i] = 0;
+      if (!paths[i] || !numpy_str_fixed(x.data(), np, s)) continue;
+      FILE *f = fopen(paths[i], "wb");
+      if (!f || fwrite(s.data(), 1, s.size(), f) != s.size()) {
+        if (f) fclose(f);
+        failed[t] = i;
+        return;
+      }
+      if (fclose(f) != 0) {
+        failed[t] = i;
+        return;
+      }
+      done[i] = 1;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto &th : pool) th.join();
+  for (unsigned t = 0; t < nt; ++t)
+    if (failed[t] >= 0)
+      return olpe::set_err(OLPE_EIO, "olpe_acceptance_write: cannot write %s", paths[failed[t]]);
   return OLPE_OK;
 }
 

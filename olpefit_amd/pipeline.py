@@ -173,6 +173,28 @@ def write_acceptance(path: str, accepts, tries) -> None:
         f.write(acceptance_text(accepts, tries))
 
 
+def write_acceptance_files(paths, accepts, tries, threads: int = 0) -> None:
+    """write_acceptance for many walkers: accepts / tries [W][P].  The native writer
+    (olpe_acceptance_write, threaded) takes the rows NumPy prints in fixed notation;
+    the others (scientific notation, a never-tried parameter's NaN) go through
+    str() here."""
+    from . import _lib
+    import ctypes as C
+    acc = np.ascontiguousarray(accepts, dtype=np.float64)
+    tr = np.ascontiguousarray(tries, dtype=np.float64)
+    n, p = acc.shape
+    if n == 0:
+        return
+    done = np.zeros(n, dtype=np.uint8)
+    arr = (C.c_char_p * n)(*[os.fsencode(x) for x in paths])
+    lib = _lib.load()
+    _lib.check(lib.olpe_acceptance_write(arr, acc.ctypes.data_as(_lib._pd),
+                                         tr.ctypes.data_as(_lib._pd), n, p, int(threads),
+                                         done.ctypes.data_as(_lib._pu8)))
+    for k in np.flatnonzero(done == 0):
+        write_acceptance(paths[k], acc[k], tr[k])
+
+
 def written_rows(count: int, burn_in: int) -> int:
     """Data rows on disk after ``count`` iterations: the reference appends a row every
     iteration with count >= burn_in but rewrites the file only when count % 10 == 0

@@ -323,9 +323,10 @@ class Output:
         (apf_step2.py:362-365, written once count >= burn_in, :342).  The reference
         rewrites them with the chain every 10 iterations; here at each checkpoint and at
         the end of the run (the count the chain files end at), so a resumed run and an
-        uninterrupted one leave the same files.  (Per launch, 65,536 walkers' files took
-        longer to format than the launch ran.)  counts: acceptance_counts() taken earlier
-        (host-only then, so it may run beside the next launch)."""
+        uninterrupted one leave the same files.  (Per launch, 65,536 walkers' NumPy prints
+        took longer than the launch ran; the native writer formats them as NumPy does.)
+        counts: acceptance_counts() taken earlier (host-only then, so it may run beside
+        the next launch)."""
         if not self.csv:
             return
         counts = counts if counts is not None else self.acceptance_counts()
@@ -333,8 +334,7 @@ class Output:
         def run(sh):
             g = self.shards.index(sh)
             tries, acc = counts[g]
-            for k, p in enumerate(self._paths(g, 1)):
-                pipeline.write_acceptance(p, acc[k], tries[k])
+            pipeline.write_acceptance_files(self._paths(g, 1), acc, tries)
         _parallel(self.shards, run)
 
     def all_sizes(self):

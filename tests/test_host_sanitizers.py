@@ -48,6 +48,27 @@ int main(int argc, char **argv) {
     fwrite(s.data(), 1, len, stdout);
     return 0;
   }
+  if (mode == "acc") {        // acc <dir> <nfiles> <np> <threads>: acceptance files
+    const std::string dir = argv[2];
+    const int nf = atoi(argv[3]), np_ = atoi(argv[4]), th = atoi(argv[5]);
+    std::vector<std::string> names;
+    std::vector<const char *> paths;
+    for (int i = 0; i < nf; ++i) names.push_back(dir + "/" + std::to_string(i) + "_acc.csv");
+    for (auto &n : names) paths.push_back(n.c_str());
+    std::vector<double> acc((size_t)nf * np_), tries((size_t)nf * np_);
+    unsigned long long x = 2463534242ull;
+    for (size_t k = 0; k < acc.size(); ++k) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      tries[k] = (double)(1 + (x >> 40) % 100000);
+      acc[k] = (double)((x >> 20) % (unsigned long long)tries[k]);
+    }
+    if (nf > 2) tries[np_] = acc[np_] = 0.0;            // row 1: NaN, left to the caller
+    std::vector<unsigned char> done(nf, 9);
+    if (olpe_acceptance_write(paths.data(), acc.data(), tries.data(), nf, np_, th, done.data()))
+      return 12;
+    for (int i = 0; i < nf; ++i) printf("%d\n", (int)done[i]);
+    return 0;
+  }
   const std::string dir = argv[2];
   const int nf = atoi(argv[3]), nr = atoi(argv[4]), nc = atoi(argv[5]), th = atoi(argv[6]);
   std::vector<std::string> names;
@@ -165,3 +186,21 @@ def test_threaded_reader_under_sanitizers(driver, tmp_path, nf, nr):
     """The reader parses in 4 MiB blocks: 2 x 20,000-row files (~8 MB each) carry lines
     across block ends; values come back bit for bit, a file of another length is an error."""
     assert _run(driver, "read", str(tmp_path), str(nf), str(nr), "17", "3").strip() == "read ok"
+
+
+def test_acceptance_writer_under_sanitizers(driver, tmp_path):
+    """olpe_acceptance_write from 5 threads: every fixed-notation row written (NumPy's
+    str() of the same ratios, byte for byte), the NaN row left to the caller."""
+    nf, npar = 23, 16
+    done = [int(v) for v in _run(driver, "acc", str(tmp_path), str(nf), str(npar), "5").split()]
+    assert done[1] == 0 and sum(done) == nf - 1
+    x = 2463534242
+    acc, tries = np.zeros(nf * npar), np.zeros(nf * npar)
+    for k in range(nf * npar):
+        x = (x * 6364136223846793005 + 1442695040888963407) % 2 ** 64
+        tries[k] = 1 + (x >> 40) % 100000
+        acc[k] = (x >> 20) % int(tries[k])
+    for i in range(nf):
+        if done[i]:
+            want = str(acc[i * npar:(i + 1) * npar] / tries[i * npar:(i + 1) * npar])
+            assert (tmp_path / f"{i}_acc.csv").read_text() == want

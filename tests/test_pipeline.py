@@ -217,6 +217,69 @@ def test_headless_step1_three_body(tmp_path):
         step1.main(argv[:7] + ["--sky", "5.9", "3.1"], three_body=True)
 
 
+def test_native_acceptance_files_equal_numpy_str(tmp_path):
+    """olpe_acceptance_write / _format (host-only) print accepts / tries as str() of the
+    float64 array does (apf_step2.py:362-365): fixed notation with NumPy's 8-digit
+    'maxprec' cut (dyadic ties included), padding and 75-column wrapping; rows NumPy
+    prints in scientific notation or with NaN fall back to str().  Bytes compared over
+    random rows of 1-40 values and a walker set mixing both kinds."""
+    import ctypes as C
+    from olpefit_amd import _lib
+    lib = _lib.load()
+
+    def native(x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        n = C.c_size_t(0)
+        _lib.check(lib.olpe_acceptance_format(x.ctypes.data_as(_lib._pd), x.size, None, 0,
+                                              C.byref(n)))
+        if n.value == 0:
+            return None
+        buf = C.create_string_buffer(n.value)
+        _lib.check(lib.olpe_acceptance_format(x.ctypes.data_as(_lib._pd), x.size, buf, n.value,
+                                              C.byref(n)))
+        return buf.raw[:n.value].decode()
+    rng = np.random.default_rng(7)
+    native_rows = 0
+    for t in range(3000):
+        p = int(rng.choice([1, 3, 16, 19, 40]))
+        k = t % 6
+        if k == 0:
+            tries = rng.integers(1, 200000, p).astype(float)
+            x = np.floor(tries * rng.random(p)) / tries
+        elif k == 1:
+            tries = rng.integers(1, 50, p).astype(float)
+            x = np.floor(tries * rng.random(p)) / tries
+        elif k == 2:
+            x = rng.integers(0, 513, p) / 512.0                # ties at the 9th digit
+        elif k == 3:
+            x = rng.random(p) * rng.choice([1, 10, 100, 1000])
+        elif k == 4:
+            x = np.round(rng.random(p), int(rng.integers(1, 10)))
+        else:
+            x = rng.random(p)
+            x[rng.random(p) < 0.3] = 0.0
+            x[rng.random(p) < 0.1] = 1.0
+        got = native(x)
+        if got is not None:
+            native_rows += 1
+            assert got == str(x), (x, got)
+    assert native_rows > 2500
+    assert native(np.array([0.5, 5e-5])) is None and native(np.array([0.5, np.nan])) is None
+    # the writer: native rows and fallbacks give the files write_acceptance gives
+    W, P = 64, 16
+    tries = rng.integers(1, 100000, (W, P)).astype(float)
+    acc = np.floor(tries * rng.random((W, P)))
+    tries[3, 5] = acc[3, 5] = 0.0                             # NaN: fallback
+    acc[7] = tries[7] * 0.5
+    acc[7, 2] = tries[7, 2] * 1e-5                            # scientific: fallback
+    a = [str(tmp_path / f"a{w}") for w in range(W)]
+    b = [str(tmp_path / f"b{w}") for w in range(W)]
+    pipeline.write_acceptance_files(a, acc, tries, threads=4)
+    for w in range(W):
+        pipeline.write_acceptance(b[w], acc[w], tries[w])
+        assert open(a[w], "rb").read() == open(b[w], "rb").read(), w
+
+
 def test_native_csv_formatter_equals_repr():
     """olpe_csv_format (host-only, no GPU) writes what csv.writer writes for float rows
     (repr of each value): edge values, random magnitudes over 10^+-30, integers, and
