@@ -821,6 +821,86 @@ def test_ragged_cutout_sizes_match_oracle(lib_loaded, n, nsrc, mode):
     s.close()
 
 
+def _random_states(n, nsrc, count, rs):
+    """Parameter vectors far from the fit: sources anywhere on (and off) the cutout,
+    narrow cores of 0.25-6 px and wide components 1-5x wider, any rotation, amplitudes
+    over three decades, ratio and background over their ranges."""
+    from olpefit_amd import synth
+    truth = np.append(synth.truth_params(n, nsrc), 0.0)
+    out = np.tile(truth, (count, 1))
+    npos = 4 if nsrc == 2 else 6
+    out[:, :npos] = rs.uniform(-0.2 * n, 1.2 * n, size=(count, npos))
+    o = npos
+    out[:, o:o + 2] = rs.uniform(-2.0, 2.0, size=(count, 2))                 # dx, dy
+    amp = slice(o + 2, o + 2 + (nsrc))
+    out[:, amp] = truth[amp] * 10 ** rs.uniform(-2, 1, size=(count, nsrc))
+    r = o + 2 + nsrc
+    out[:, r] = rs.uniform(0.0, 1.0, size=count)                             # ratio
+    out[:, r + 1] = rs.uniform(1.0, 100.0, size=count)                       # bkgd
+    sx = r + 2
+    out[:, sx:sx + 2] = rs.uniform(0.25, 6.0, size=(count, 2))               # narrow
+    out[:, sx + 2:sx + 4] = out[:, sx:sx + 2] * rs.uniform(1.0, 5.0, size=(count, 2))
+    out[:, sx + 4:sx + 6] = rs.uniform(-np.pi, np.pi, size=(count, 2))       # thetas
+    return out
+
+
+@pytest.mark.parametrize("n,nsrc", [(64, 2), (64, 3), (128, 3), (33, 2)])
+@pytest.mark.parametrize("mode", MODES)
+def test_random_states_chi2_matches_oracle(golden, lib_loaded, n, nsrc, mode):
+    """olpe_chi2_batch on 1,500 parameter vectors far from the fit (every FAST guard
+    level and fallback the grid allows) against the oracle at the stated tolerances."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    img, _ = synth.make_image(n, nsrc, 2)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    P = _random_states(n, nsrc, 1500, np.random.RandomState(n + nsrc))
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode(mode)
+    got = s.chi_squared(P)
+    s.close()
+    with np.errstate(all="ignore"):
+        ref = np.array([float(ora.chi_squared(dm, ora.build_analytical_model(p, n, nsrc), err))
+                        for p in P])
+    fin = np.isfinite(ref)
+    assert fin.sum() > 1000 and np.array_equal(np.isfinite(got), fin)
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=TOL[mode]["chi"], atol=0)
+
+
+@pytest.mark.parametrize("n,nsrc", [(64, 2), (64, 3), (128, 3)])
+def test_random_states_sampler_proposals_match_oracle(golden, lib_loaded, n, nsrc):
+    """The bench samplers' sweeps (64x64 LDS kernels, the 128x128 ring) from 1,024
+    walkers at random states far from the fit: one traced iteration each, the
+    proposal's chi^2 against the oracle's for the same vector (FAST tolerance)."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    img, _ = synth.make_image(n, nsrc, 2)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    W = 1024
+    P = _random_states(n, nsrc, W, np.random.RandomState(7 * n + nsrc))
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode("fast")
+    P[:, -1] = s.chi_squared(P)
+    s.seed(np.arange(900, 900 + W))
+    s.set_state(P)
+    s.enable_trace(True)
+    s.run(1, burn_in=0, record_stride=0)
+    tr = s.trace(1)[:, 0, :]
+    s.close()
+    checked = 0
+    for w in range(W):
+        r, new, chi = int(tr[w, 0]), tr[w, 1], tr[w, 2]
+        q = P[w].copy()
+        q[r] = new
+        with np.errstate(all="ignore"):
+            ref = float(ora.chi_squared(dm, ora.build_analytical_model(q, n, nsrc), err))
+        if not np.isfinite(ref):
+            assert not np.isfinite(chi)
+            continue
+        assert abs(chi - ref) <= TOL["fast"]["chi"] * abs(ref), (w, r, chi, ref)
+        checked += 1
+    assert checked > 800
+
+
 @pytest.mark.parametrize("n,nsrc,mode", [(1024, 2, "fast"), (900, 3, "exact"), (600, 2, "exact")])
 def test_full_frame_cutouts_match_oracle(lib_loaded, n, nsrc, mode):
     """Frames far beyond the cutout sizes of the bench (a full 1024 x 1024 NIRC2 frame):
