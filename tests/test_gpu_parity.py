@@ -901,6 +901,33 @@ def test_random_states_sampler_proposals_match_oracle(golden, lib_loaded, n, nsr
     assert checked > 800
 
 
+@pytest.mark.parametrize("n,nsrc", [(64, 2), (128, 3)])
+def test_random_states_trajectories_match_oracle(golden, lib_loaded, n, nsrc):
+    """48 walkers started at random states far from the fit, 150 iterations each
+    through the bench sampler (FAST): as the chains move, steps pass between FAST3 and
+    the fallback sweeps; every recorded state against the oracle's trajectory."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    img, _ = synth.make_image(n, nsrc, 3)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    W, it = 48, 150
+    P = _random_states(n, nsrc, W, np.random.RandomState(11 * n + nsrc))
+    with np.errstate(all="ignore"):
+        for p in P:
+            p[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p, n, nsrc), err))
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode("fast")
+    seeds = np.arange(700, 700 + W)
+    s.seed(seeds)
+    s.set_state(P)
+    chain = s.run(it, burn_in=0, record_stride=1)
+    s.close()
+    for w in range(W):
+        ref, _ = ora.Walker(dm, err, P[w], int(seeds[w]), nsrc=nsrc).run(it)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9,
+                                   err_msg=f"walker {w}")
+
+
 @pytest.mark.parametrize("n,nsrc,mode", [(1024, 2, "fast"), (900, 3, "exact"), (600, 2, "exact")])
 def test_full_frame_cutouts_match_oracle(lib_loaded, n, nsrc, mode):
     """Frames far beyond the cutout sizes of the bench (a full 1024 x 1024 NIRC2 frame):
