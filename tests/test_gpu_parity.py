@@ -901,6 +901,28 @@ def test_random_states_sampler_proposals_match_oracle(golden, lib_loaded, n, nsr
     assert checked > 800
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_mcds_header_noise_model_matches_oracle(lib_loaded, mode):
+    """A frame read out in MCDS (sampmode 3: saturation scaled by multisam / itime,
+    readnoise 38 / sqrt(multisam) x sqrt(coadds), apf_step2.py:182-204) with coadds 5:
+    the library's chi^2 over the random-state vectors equals the oracle's."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    img, _ = synth.make_image(64, 2, 5)
+    img = img * 4.0
+    dm, err, _, _ = ora.noise_model(img, 30.0, 5, 8, 3)
+    assert 0 < np.ma.count_masked(dm) < 100             # the star's peak saturates
+    P = _random_states(64, 2, 200, np.random.RandomState(5))
+    s = Sampler(img, 30.0, 5, 8, 3, nsrc=2)
+    s.set_eval_mode(mode)
+    got = s.chi_squared(P)
+    s.close()
+    with np.errstate(all="ignore"):
+        ref = np.array([float(ora.chi_squared(dm, ora.build_analytical_model(p, 64, 2), err))
+                        for p in P])
+    np.testing.assert_allclose(got, ref, rtol=TOL[mode]["chi"], atol=0)
+
+
 @pytest.mark.parametrize("n,nsrc", [(64, 2), (128, 3)])
 def test_random_states_trajectories_match_oracle(golden, lib_loaded, n, nsrc):
     """48 walkers started at random states far from the fit, 150 iterations each

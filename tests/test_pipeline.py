@@ -217,6 +217,25 @@ def test_headless_step1_three_body(tmp_path):
         step1.main(argv[:7] + ["--sky", "5.9", "3.1"], three_body=True)
 
 
+@pytest.mark.parametrize("sampmode", [2, 3, 1])
+def test_noise_model_header_cases_equal_oracle(sampmode):
+    """apf_step2.py:176-210 for the header values the reference branches on: sampmode 3
+    (MCDS: saturation scaled by multisam / itime, readnoise 38 / sqrt(multisam)), 2
+    (CDS) and any other; coadds and multisam > 1; float32 and float64 frames.  The
+    product's mask and err equal the oracle's (masked_greater's mask; err bit for bit)."""
+    from olpefit_amd import core, synth
+    from oracle import olpe_oracle as ora
+    img32, _ = synth.make_image(48, 2, 4)
+    for img in (img32, img32.astype(np.float64) * 1.7):
+        for coadds, multisam, itime in ((1, 1, 1.0), (5, 8, 0.25), (10, 16, 30.0), (2, 2, 0.05)):
+            mask, pois2, rn2, sat, rn = core.noise_model(img, itime, coadds, multisam, sampmode)
+            dm, err, sat_o, rn_o = ora.noise_model(img, itime, coadds, multisam, sampmode)
+            assert sat == sat_o and rn == rn_o
+            np.testing.assert_array_equal(mask, np.ma.getmaskarray(dm))
+            got = np.sqrt(rn2 + pois2.astype(np.float64))
+            assert np.array_equal(got, err)
+
+
 def test_native_acceptance_files_equal_numpy_str(tmp_path):
     """olpe_acceptance_write / _format (host-only) print accepts / tries as str() of the
     float64 array does (apf_step2.py:362-365): fixed notation with NumPy's 8-digit
