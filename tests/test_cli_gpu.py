@@ -191,6 +191,30 @@ def test_cli_three_source_feeds_step3(tmp_path):
             np.testing.assert_allclose(summ[name][key], r[key], rtol=1e-12, err_msg=(name, key))
 
 
+def test_headless_three_source_pipeline(tmp_path):
+    """3body step 1 (headless: 8x8 aperture, integer positions) -> 3body step 2 (its
+    initial guess read from step 1's file, 3body/apf_step2_3body.py:255-265) -> 3body
+    step 3: the chains start at step 1's positions and step 3 reads them."""
+    from olpefit_amd import step1
+    path = synth.write_case(str(tmp_path), 64, 3)
+    t = synth.truth_params(64, 3)
+    gp = step1.main([str(tmp_path), "--star", str(t[0] + 1.2), str(t[1] - 0.7),
+                     "--companion", str(t[2] - 0.4), str(t[3] + 1.1),
+                     "--companion", str(t[4] + 0.6), str(t[5] + 0.3),
+                     "--sky", "4", "5"], three_body=True)
+    guess = pipeline.read_guess(gp[0])
+    assert len(guess) == 8 and np.all(guess == np.round(guess))
+    out = step2.main([path, "--walkers", "4", "--seed", "5", "--iters", "100", "-q"], nsrc=3)
+    c = step3.load_chains(out, 4, additional_burnin=1)
+    assert c.shape == (100, 4, 20) and np.all(np.isfinite(c))
+    # the first recorded state is one Gibbs step from the initial vector: at most one
+    # parameter moved, so at most one of the six positions differs from step 1's
+    moved = np.sum(c[0, :, :6] != guess[None, :6], axis=1)
+    assert np.all(moved <= 1), c[0, :, :6]
+    cli = step3.main([path, "system", "-s", "4", "-q"], nsrc=3)
+    assert cli["walkers"] == 4 and len(cli["parameters"]) == 19
+
+
 @pytest.mark.parametrize("mode", ["iters", "accept_min"])
 def test_cli_resume_after_interrupt(tmp_path, monkeypatch, mode):
     """A run killed after a launch's rows reached the files but before its checkpoint
