@@ -635,9 +635,22 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       // (per-column guard cache: the Gaussians this draw moves or reshapes -- a shape
       // set is the narrow Gaussians, odd g, or the wide ones, even g)
       gcache.changed = gmask | ((grp == 1 ? 0xAAAu : grp == 2 ? 0x555u : 0u) & ((1u << (2 * NSRC)) - 1u));
-      const double part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
-                                                       &hcache, &ccache, gmask, &gcache,
-                                                       RING ? &ring : nullptr);
+      // A NaN proposal (logproposal of a value <= 0, apf_step2.py:66-69: a background
+      // guessed below 0 proposes NaN at every draw of it) makes the reference's model NaN
+      // at every pixel, its masked chi^2 NaN and the step a reject (:134-148): no sweep
+      // (the guards would send it to the exact sweep, and in the ring sampler hold up
+      // the workgroup), the caches left as they are.
+      const bool nan_prop = !(nv == nv);
+      double part;
+      if (nan_prop) {
+        gcache.same = false;
+        if constexpr (RING) ring.idle_step();
+        part = __builtin_nan("");
+      } else {
+        part = sweep<NSRC, NT, false, FAST, (WPB <= 12), Ring>(*mdl, DE, vtab, nullptr, n, lane, etab,
+                                                     &hcache, &ccache, gmask, &gcache,
+                                                     RING ? &ring : nullptr);
+      }
       __builtin_amdgcn_s_setprio(RING && OLPE_RING_PRIO_STEP > 1 ? 3 : OLPE_CTRL_PRIO);
       DT_MARK(3);
       // (the total is valid in lane 63: the accept ballots that lane's test, and lane 63

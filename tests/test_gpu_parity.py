@@ -901,6 +901,45 @@ def test_random_states_sampler_proposals_match_oracle(golden, lib_loaded, n, nsr
     assert checked > 800
 
 
+@pytest.mark.parametrize("n,nsrc,wpb", [(64, 2, "16"), (64, 2, "12"), (64, 3, "12"),
+                                         (128, 2, "12"), (128, 3, "12"), (40, 2, "12")])
+@pytest.mark.parametrize("mode", MODES)
+def test_nan_proposals_rejected_without_sweep(lib_loaded, monkeypatch, n, nsrc, wpb, mode):
+    """A background guessed below 0 (a sky box whose median is negative): every draw of
+    it is a log-normal proposal of a negative value, NaN (apf_step2.py:66-69), which the
+    reference rejects through its NaN chi^2.  The sampler skips the sweep for such
+    proposals (in the 128x128 ring the wave only keeps the phases): the traced chi^2 is
+    NaN on exactly those steps and the chains equal the oracle's."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    monkeypatch.setenv("OLPE_WPB", wpb)
+    img, truth = synth.make_image(n, nsrc, 6)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = np.append(truth, 0.0)
+    bk = 9 if nsrc == 2 else 12
+    p0[bk] = -3.5
+    with np.errstate(all="ignore"):
+        p0[-1] = float(ora.chi_squared(dm, ora.build_analytical_model(p0, n, nsrc), err))
+    W, it = 16, 200
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode(mode)
+    seeds = np.arange(300, 300 + W)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (W, 1)))
+    s.enable_trace(True)
+    chain = s.run(it, burn_in=0, record_stride=1)
+    tr = s.trace(it)
+    s.close()
+    nan_steps = 0
+    for w in range(W):
+        ref, rtr = ora.Walker(dm, err, p0, int(seeds[w]), nsrc=nsrc).run(it, trace=True)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL[mode]["traj"], atol=1e-9)
+        drawn_bk = tr[w, :, 0] == bk
+        assert np.all(np.isnan(tr[w, drawn_bk, 2])) and not np.any(tr[w, drawn_bk, 5] > 0.5)
+        nan_steps += int(drawn_bk.sum())
+    assert nan_steps > 0 and np.all(chain[:, :, bk] == -3.5)
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_mcds_header_noise_model_matches_oracle(lib_loaded, mode):
     """A frame read out in MCDS (sampmode 3: saturation scaled by multisam / itime,

@@ -1,7 +1,7 @@
 """Which sweep the sampler's steps take (diagnostic build only):
 
     tools/diag_build.sh fb -DOLPE_DIAG_FALLBACK
-    OLPE_LIB=diag/fb/libolpe.so python tools/diag_fallback.py [config]
+    OLPE_LIB=diag/fb/libolpe.so python tools/diag_fallback.py [config | n nsrc walkers]
 
 Runs bench.py's workload for one config (a few 100-iteration launches) and prints the
 share of walker-steps that took the FAST3 sweep, and of the fallbacks (FAST2, V table,
@@ -21,8 +21,12 @@ def main():
     from olpefit_amd import _lib, synth
     from olpefit_amd.core import Sampler
     from olpefit_amd.pipeline import initial_parameters
-    cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    W, n, nsrc = bench.CONFIGS[cfg]
+    if len(sys.argv) > 3:                 # any shape: n nsrc walkers
+        n, nsrc, W = (int(v) for v in sys.argv[1:4])
+        cfg = f"{n}x{n}/{nsrc}"
+    else:
+        cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+        W, n, nsrc = bench.CONFIGS[cfg]
     img, _ = synth.make_image(n, nsrc, 0)
     s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
