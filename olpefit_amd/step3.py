@@ -73,7 +73,8 @@ def gelman_rubin(p, d: int = 16):
     19 by 17 as integers: the factor is 1 and RC = sqrt(PSRF).  Integer ``d`` keeps
     that floor division here; a float ``d`` divides as floats, as it would there."""
     p = np.asarray(p, dtype=np.float64)
-    N, M = float(p.shape[0]), float(p.shape[1])
+    # (NumPy floats: one walker gives NaN, as summary_from_moments does, not a raise)
+    N, M = np.float64(p.shape[0]), np.float64(p.shape[1])
     overall_mean = np.mean(p)
     # the reference's per-column loop (np.mean / np.std of p[:, i]) as row reductions of
     # the transpose: the same pairwise sums over the same values, so the same bits
@@ -212,6 +213,10 @@ def main(argv=None, nsrc: int = 2):
         say('Importing parameter arrays...')                        # :167
         chains = load_chains(input_directory, ncor, 0, source="npy" if args.npy else "csv")
         length = chains.shape[0]
+        if length - additional_burnin < 1:
+            raise ValueError(f"{input_directory}: {length} rows per walker file, none left "
+                             f"after additional_burnin = {additional_burnin} (step 2's "
+                             f"burn-in may exceed its run)")
         say('Parameter array shape:', length)                       # :172
         chains = chains[additional_burnin:length]                   # :190-205
         stats = summary(chains, nsrc)

@@ -496,3 +496,7 @@ def test_step3_cli_reads_step2_output(tmp_path, golden, capsys):
         np.testing.assert_allclose(mom["parameters"][k]["gr_rc"], r["gr_rc"], rtol=5e-12)
     with pytest.raises(ValueError):
         step3.main([image, "x", "-s", str(M + 1), "--from-moments", "-q"])
+    # a step-2 run shorter than its burn-in leaves only the NaN seed row: a clear error
+    pipeline.write_chain_csvs(paths, np.zeros((M, 0, ps)), nan_row=True)
+    with pytest.raises(ValueError, match="none left"):
+        step3.main([image, "x", "-s", str(M), "-q"])
