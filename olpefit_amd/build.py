@@ -3,6 +3,7 @@ the repo snapshot to the GPU box)."""
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -49,17 +50,23 @@ def _elf_section(path: str, name: str) -> bytes:
 def kernel_digest(lib: str = LIB) -> str:
     """16 hex digits identifying the sampler's device code: tags measured per-kernel
     counts (profiles/valu_counts.json) with the code they were measured on.  It is the
-    hash of the built library's device code objects (its .hip_fatbin section: the same
-    bytes whenever the device code is the same -- an edit to host code, a comment or a
-    diagnostic build's hook leaves it unchanged); without a library, the hash of the
-    flags and the device sources' text."""
+    hash of the built library's code-object bundles that hold the sampler kernel (its
+    .hip_fatbin section has one clang offload bundle per HIP source: the same bytes
+    whenever that source's device code is the same -- an edit to host code, a comment,
+    a diagnostic build's hook or another source's kernels (olpe_moments.hip) leaves it
+    unchanged); without a library, the hash of the flags and the device sources'
+    text."""
     import hashlib
     try:
         fat = _elf_section(lib, ".hip_fatbin")
     except OSError:
         fat = None
     if fat:
-        return hashlib.sha256(b"fatbin:" + fat).hexdigest()[:16]
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), fat)]
+        bundles = [fat[a:b] for a, b in zip(starts, starts[1:] + [len(fat)])] or [fat]
+        mine = [b for b in bundles if b"olpe_gibbs_kernel" in b] or bundles
+        return hashlib.sha256(b"fatbin:" + b"".join(mine)).hexdigest()[:16]
     h = hashlib.sha256(" ".join(FLAGS).encode())
     for f in ("olpe.hip", "olpe_device.h", "exp_table.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
