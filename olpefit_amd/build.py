@@ -47,6 +47,17 @@ def _elf_section(path: str, name: str) -> bytes:
     return None
 
 
+def fatbin_digest(fat: bytes, kernel: bytes = b"olpe_gibbs_kernel") -> str:
+    """kernel_digest of a .hip_fatbin section: the hash of the clang offload bundles
+    that name `kernel` (all of them if none does)."""
+    import hashlib
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), fat)]
+    bundles = [fat[a:b] for a, b in zip(starts, starts[1:] + [len(fat)])] or [fat]
+    mine = [b for b in bundles if kernel in b] or bundles
+    return hashlib.sha256(b"fatbin:" + b"".join(mine)).hexdigest()[:16]
+
+
 def kernel_digest(lib: str = LIB) -> str:
     """16 hex digits identifying the sampler's device code: tags measured per-kernel
     counts (profiles/valu_counts.json) with the code they were measured on.  It is the
@@ -62,11 +73,7 @@ def kernel_digest(lib: str = LIB) -> str:
     except OSError:
         fat = None
     if fat:
-        magic = b"__CLANG_OFFLOAD_BUNDLE__"
-        starts = [m.start() for m in re.finditer(re.escape(magic), fat)]
-        bundles = [fat[a:b] for a, b in zip(starts, starts[1:] + [len(fat)])] or [fat]
-        mine = [b for b in bundles if b"olpe_gibbs_kernel" in b] or bundles
-        return hashlib.sha256(b"fatbin:" + b"".join(mine)).hexdigest()[:16]
+        return fatbin_digest(fat)
     h = hashlib.sha256(" ".join(FLAGS).encode())
     for f in ("olpe.hip", "olpe_device.h", "exp_table.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:

@@ -131,3 +131,20 @@ def test_wpb_knob_is_validated_against_the_lds(lib, monkeypatch):
         monkeypatch.setenv("OLPE_WPB", wpb)
         if not n.value:
             assert create() == _lib.EHIP        # valid knob: fails only for lack of a GPU
+
+
+def test_kernel_digest_covers_only_the_sampler_bundle():
+    """The VALU counts in profiles/ are tagged with the hash of the sampler's code-object
+    bundle only: another source's kernels (olpe_moments.hip) may change without marking
+    them stale, a change inside the sampler's bundle does; the built library's digest is
+    the one its section gives."""
+    from olpefit_amd.build import fatbin_digest, kernel_digest, _elf_section, LIB
+    m = b"__CLANG_OFFLOAD_BUNDLE__"
+    a = m + b"..olpe_gibbs_kernel..code-A.."
+    b = m + b"..fold_kernel..code-B.."
+    ref = fatbin_digest(a + b)
+    assert fatbin_digest(a + m + b"..fold_kernel..code-B2..") == ref
+    assert fatbin_digest(m + b"..olpe_gibbs_kernel..code-A2.." + b) != ref
+    assert fatbin_digest(b"no bundles") != ref
+    if os.path.exists(LIB):
+        assert kernel_digest() == fatbin_digest(_elf_section(LIB, ".hip_fatbin"))
