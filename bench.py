@@ -44,17 +44,29 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # BASELINE.json configs -> (walkers per GPU, image side, nsrc)
-# (keys are BASELINE.json config indices; [0] is the 1-walker CPU plumbing case and
-# [3] is configs[2] sharded over 8 GPUs, i.e. this bench at --gpus 8)
+# (keys are BASELINE.json config indices; [3] is configs[2] sharded over 8 GPUs, i.e.
+# this bench at --gpus 8)
 CONFIGS = {
+    0: (1, 32, 2),
     1: (4096, 64, 2),
     2: (65536, 64, 2),
     4: (16384, 128, 3),
 }
 CONFIG_NAMES = {
+    0: "configs[0]: 1 walker, 32x32 2-source cutout, 1,000 iterations (plumbing reference)",
     1: "configs[1]: 4,096 walkers, 64x64 2-source cutout, fp64",
     2: "configs[2]: 65,536 walkers/GPU, 64x64 2-source cutout, fp64, LDS-resident image",
     4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
+}
+# SURVEY.md 8(d)'s run of each config: iterations per launch (a bench step), chain record
+# stride ("every step for configs 1-2 and with stride 10 otherwise"), timed steps and
+# warm-up steps, so that the timed steps cover the config's iteration count: configs[0]
+# 1,000 iterations, configs[1] 10,000, configs[2] 2,000, configs[4] 500
+DEFAULTS = {
+    0: dict(iters=1000, stride=1, steps=1, warmup=1),
+    1: dict(iters=1000, stride=1, steps=10, warmup=2),
+    2: dict(iters=100, stride=10, steps=20, warmup=5),
+    4: dict(iters=100, stride=10, steps=5, warmup=2),
 }
 # BASELINE.json's metric, character for character (its "64\u00d764")
 METRIC = "walker-steps/sec (= model evals/sec) on 64\u00d764 2-source cutout, 1/2/4/8 GPU"
@@ -171,10 +183,12 @@ def host_cpus():
     return cores, aff, quota, model or platform.processor()
 
 
-def cpu_baseline(n: int, nsrc: int, total_iters: int):
+def cpu_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None):
     """The oracle (one walker per process, like one MPI rank per walker) on every core
-    this job may use, ``total_iters`` walker-steps in all (about 12 s of CPU work)."""
-    procs, aff, quota, model = host_cpus()
+    this job may use (or ``procs`` processes), ``total_iters`` walker-steps in all (about
+    12 s of CPU work)."""
+    cores, aff, quota, model = host_cpus()
+    procs = procs or cores
     iters = max(200, total_iters // procs)
     with mp.get_context("spawn").Pool(procs) as pool:
         pool.map(_cpu_worker, [(n, nsrc, 1, 5)] * procs)          # import warm-up
@@ -184,11 +198,28 @@ def cpu_baseline(n: int, nsrc: int, total_iters: int):
     steps = procs * iters
     return {"value": steps / wall, "unit": "walker-steps/s", "cores": procs, "kind": "port",
             "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_model": model,
-            "sample": f"oracle/olpe_oracle.py NumPy restatement, {procs} processes (one per "
-                      f"usable core: affinity {aff} CPUs, cgroup quota "
+            "sample": f"oracle/olpe_oracle.py NumPy restatement, {procs} processes ("
+                      f"{'one per usable core' if procs == cores else 'of the usable cores'}: "
+                      f"affinity {aff} CPUs, cgroup quota "
                       f"{'none' if quota is None else f'{quota:g}'}) x 1 walker x {iters} "
                       f"iterations, {n}x{n} {nsrc}-source cutout ({sum(times):.1f} s CPU); "
                       f"cpu: {model}"}
+
+
+def reference_ratio(n: int, nsrc: int, path: str):
+    """The reference's own apf_step2 loop against the port on one core of the build
+    container (tests/golden/time_reference.py --json; the reference cannot travel to the
+    GPU box): ``reference_over_port`` = the reference's iterations/s / the port's (< 1:
+    the reference is slower).  None without a timing for this shape."""
+    data = load_json(path) or {}
+    ent = data.get(f"{n}x{n}_{nsrc}")
+    if not ent:
+        return None
+    return {"reference_over_port": ent["reference_over_port"],
+            "reference_iters_per_s_one_core": ent["reference_iters_per_s"],
+            "port_iters_per_s_one_core": ent["port_iters_per_s"],
+            "timing_cpu": ent["cpu_model"], "timing_iterations": ent["iterations"],
+            "timing_file": os.path.relpath(path, REPO)}
 
 
 def _comm_timeout(rank: int, make_report, timeout: float):
@@ -213,18 +244,108 @@ def load_json(path: str):
         return None
 
 
+def sampler_class():
+    """The per-GPU sampler, ``olpefit_amd.core.Sampler`` (libolpe.so).  The CPU tests of
+    the launcher and of the N > 1 reporting set OLPE_BENCH_SAMPLER=module:Class to a
+    stand-in that runs no kernel (tests/bench_stub.py); the product has no other."""
+    spec = os.environ.get("OLPE_BENCH_SAMPLER")
+    if spec:
+        import importlib
+        mod, _, cls = spec.partition(":")
+        return getattr(importlib.import_module(mod), cls)
+    from olpefit_amd.core import Sampler
+    return Sampler
+
+
+# ----------------------------------------------------------------------------------
+# rank launcher: `bench.py --gpus N` without a launcher's environment
+# ----------------------------------------------------------------------------------
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, grace_s: float = 30.0) -> int:
+    """Start ``n`` ranks of this script (one process per GPU, LOCAL_RANK = device) and
+    relay rank 0's output -- the reference's launch-sized world (``mpiexec -n W python
+    apf_step2.py``, apf_step2.py:27-29, :50-57) without an external launcher.
+
+    The parent makes no HIP call (it imports neither libolpe nor the sampler), so the
+    children own the GPUs.  Rank 0's stdout (the JSON line) is copied to this stdout; the
+    other ranks' stdout and every rank's stderr go to this stderr.  Returns 0 if every
+    rank exits 0, else the first non-zero status; when a rank fails, the others get
+    ``grace_s`` to finish (a rank blocked in the host group on a dead peer would wait for
+    its timeout) and are then terminated -- only the processes started here."""
+    import subprocess
+    env0 = dict(os.environ)
+    port = _free_port()
+    env0.update(MASTER_ADDR=env0.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port),
+                WORLD_SIZE=str(n), OLPE_BENCH_LAUNCHED="1")
+    env0.setdefault("TORCHELASTIC_RUN_ID", f"bench-{os.getpid()}-{port}")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                      stderr=None, text=True))
+
+    def pump():
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    status = 0
+    deadline = None
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0:
+                print(f"[bench launcher] rank {r} exited with status {rc}", file=sys.stderr)
+                if status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    deadline = time.monotonic() + grace_s
+        if live and deadline is not None and time.monotonic() > deadline:
+            for r in sorted(live):
+                print(f"[bench launcher] terminating rank {r} after a peer failed",
+                      file=sys.stderr)
+                procs[r].terminate()
+            for r in sorted(live):
+                try:
+                    procs[r].wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    procs[r].kill()
+                    procs[r].wait()
+            live.clear()
+        time.sleep(0.05)
+    t.join(timeout=10)
+    return status
+
+
 # ----------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU, default 1).  Without a launcher's "
+                         "WORLD_SIZE, N > 1 starts the N ranks itself; under torchrun / "
+                         "mpirun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=None,
-                    help="timed steps (default 10; 200 for --config 1, see below)")
+                    help="timed steps (default: the config's, DEFAULTS)")
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed steps first (default 2; 50 for --config 1)")
+                    help="untimed steps first (default: the config's, DEFAULTS)")
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--walkers", type=int, default=0, help="override walkers per GPU")
-    ap.add_argument("--iters", type=int, default=100, help="Gibbs iterations per step")
-    ap.add_argument("--stride", type=int, default=10, help="chain record stride")
+    ap.add_argument("--iters", type=int, default=None,
+                    help="Gibbs iterations per step (default: the config's, DEFAULTS)")
+    ap.add_argument("--stride", type=int, default=None,
+                    help="chain record stride (default: the config's, DEFAULTS)")
     ap.add_argument("--mode", default="fast", choices=["exact", "fast"])
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the single-GPU measurement of the other eval mode")
@@ -234,6 +355,8 @@ def main():
                          "64^2/n^2 otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--reference-timing",
+                    default=os.path.join(REPO, "profiles", "r04", "reference_cpu_timing.json"))
     ap.add_argument("--valu", default=os.path.join(REPO, "profiles", "valu_counts.json"))
     ap.add_argument("--gather-mib", type=float, default=1024.0,
                     help="N > 1: MiB of chain rows per rank per all-gather range")
@@ -256,15 +379,22 @@ def main():
                          "and the RCCL exchange attempted (RCCL refuses it; the line "
                          "carries comm_error)")
     args = ap.parse_args()
-    # configs[1]'s launch is ~0.85 ms: the chip raises its clock only under sustained
-    # load (in-kernel s_memtime/s_memrealtime: ~1.9 GHz over the first ~10 ms of work,
-    # ~2.17 GHz sustained), so its default run is long enough to measure
-    # the sustained rate (250 launches, 0.2 s) like the 12 ms launches of configs[2]
-    short = args.config == 1
-    if args.steps is None:
-        args.steps = 200 if short else 10
-    if args.warmup is None:
-        args.warmup = 50 if short else 2
+    if args.gpus is not None and args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            # no launcher: this process starts the ranks and makes no HIP call itself
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif args.gpus is not None and int(env_world) != args.gpus:
+        ap.error(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+    dflt = DEFAULTS[args.config]
+    for k in ("iters", "stride", "steps", "warmup"):
+        if getattr(args, k) is None:
+            setattr(args, k, dflt[k])
+    # the per-config default shape (the profiled one: profiles/valu_counts.json)
+    default_shape = not args.walkers and args.iters == dflt["iters"] \
+        and args.stride == dflt["stride"]
 
     from olpefit_amd import dist as odist
     rank, world, local = odist.env()
@@ -272,14 +402,17 @@ def main():
     barrier, allmax = group.barrier, group.allmax
 
     from olpefit_amd import synth
-    from olpefit_amd.core import Sampler
+    Sampler = sampler_class()
 
     wpg, n, nsrc = CONFIGS[args.config]
     if args.walkers:
         wpg = args.walkers
     img, _ = synth.make_image(n, nsrc, 0)
     shared = args.share_gpu or args.share_gpu_rccl
-    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=0 if shared else local)
+    device = 0 if shared else local
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=device)
+    # which process / device each rank is (the line names them: one process per GPU)
+    placement = group.allgather([rank, local, device, os.getpid()])
     # step-1 style start (apf_step2.py:264-289) for every walker
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
@@ -336,7 +469,6 @@ def main():
         valu = load_json(args.valu) or {}
         from olpefit_amd.build import kernel_digest
         digest = kernel_digest()
-        default_shape = not args.walkers and args.iters == 100 and args.stride == 10
 
         def key(mode):
             return mode if args.config == 2 else f"c{args.config}_{mode}"
@@ -418,7 +550,12 @@ def main():
                        "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                        "chain_stride": args.stride, "eval": args.mode,
                        "chunks_per_walker": units,
-                       "parallelism": f"walker-sharded x{world}"},
+                       "parallelism": f"walker-sharded x{world}",
+                       "devices": [p[2] for p in placement],
+                       "local_ranks": [p[1] for p in placement],
+                       "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
+                                    else "environment" if "WORLD_SIZE" in os.environ
+                                    else "none (1 rank)")},
             "roofline": roofline(args.mode, kernel_ms),
             "acceptance": acceptance,
             "allgather_ms": None,
@@ -498,6 +635,15 @@ def main():
             print(f"[bench rank {rank}] RCCL exchange failed: {comm['comm_error']}",
                   file=sys.stderr)
 
+    if world > 1 and args.share_gpu and not args.no_moments:
+        # ranks sharing one GPU have no RCCL: their moments are summed over the host
+        # group instead (the two rounds of olpe_comm_allreduce_moments: the pooled mean,
+        # then the squared deviations about it; step3.combine_moments)
+        from olpefit_amd import step3
+        parts = group.allgather(s.moments_summary().tolist())
+        cparts = group.allgather(s.moments_summary(step3.pooled_mean(parts)).tolist())
+        moments = step3.combine_moments(parts, cparts)
+
     if rank != 0:
         watchdog_cancel()
         s.close()
@@ -514,18 +660,35 @@ def main():
         from olpefit_amd import step3
         summ = step3.summary_from_moments(moments, nsrc)
         names = step3.NAMES_2 if nsrc == 2 else step3.NAMES_3
+        rc = [summ[k]["gr_rc"] for k in names[:-1]]
         out["posterior"] = {
             "rows_per_walker": summ["_rows_per_walker"], "walkers": summ["_walkers"],
             "means": {k: summ[k]["mean"] for k in names[:4]},
             "stds": {k: summ[k]["std"] for k in names[:4]},
-            "gr_rc_max": max(summ[k]["gr_rc"] for k in names[:-1]),
+            # Gelman-Rubin needs two walkers or more (configs[0] has one: null)
+            "gr_rc_max": max(rc) if all(np.isfinite(rc)) else None,
             "acceptance": sum(summ[k]["accepts"] for k in names[:-1])
             / sum(summ[k]["tries"] for k in names[:-1])}
     value = out["value"]
     if not args.no_cpu_baseline and world == 1:
         cpu_steps = args.cpu_steps or max(4000, 96000 * 64 * 64 // (n * n))
-        out["cpu_baseline"] = cpu_baseline(n, nsrc, cpu_steps)
-        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        # configs[0] is the one-walker plumbing case: the GPU's one walker beside the
+        # oracle's one walker on one core, the reference's 1,000 iterations
+        cb = (cpu_baseline(n, nsrc, args.cpu_steps or 1000, procs=1) if args.config == 0
+              else cpu_baseline(n, nsrc, cpu_steps))
+        out["cpu_baseline"] = cb
+        out["gpu_over_cpu"] = value / cb["value"]
+        ref = reference_ratio(n, nsrc, args.reference_timing)
+        if ref:
+            # the reference itself is slower than the port on the same core: its rate on
+            # these cores, derived from the ratio measured in the build container
+            cb.update(ref)
+            cb["reference_value_derived"] = cb["value"] * ref["reference_over_port"]
+            out["gpu_over_reference"] = value / cb["reference_value_derived"]
+            out["gpu_over_reference_note"] = (
+                "derived: cpu_baseline.value x reference_over_port, the reference/port "
+                "speed ratio measured on one core of the build container "
+                "(profiles/r04/reference_cpu_timing.json), not on this box")
     print(json.dumps(out))
     s.close()
     group.close()

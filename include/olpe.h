@@ -217,14 +217,20 @@ int olpe_comm_allgather_state(olpe_ctx *ctx, double *out);
  * collective alone).  Gathering a large ensemble range by range bounds both the device
  * receive buffer and the host buffer by the range.  *nrec_out (may be NULL) = nrec.
  * Every rank must call with the same range and have the same W and nrec (checked:
- * OLPE_EINVAL on every rank otherwise). */
+ * OLPE_EINVAL on every rank otherwise).  The receive buffer is allocated before that
+ * check and its outcome travels with it: a rank that cannot allocate it (or whose
+ * olpe_comm_gather_limit it exceeds) makes the call OLPE_ENOMEM on every rank. */
 int olpe_comm_allgather_chain(olpe_ctx *ctx, long long w0, long long wn, double *out,
                               long long *nrec_out);
+/* Byte limit of the chain gather's device receive buffer (nranks x range bytes; 0 = no
+ * limit, the default): a memory budget for the gather, like bench.py's --gather-mib. */
+int olpe_comm_gather_limit(olpe_ctx *ctx, long long bytes);
 /* Posterior summary over every rank from the whole-run moments (olpe_moments_*): two
  * all-reduces (sum), the pooled mean first, then the deviations of the walkers' means
  * about it.  out[OLPE_MOMENTS_LEN(PS, P)] as for olpe_moments_summary, over all ranks'
  * walkers, with centre = the pooled mean (out[2 + k] / out[1]).  Every rank must have
- * folded the same number of rows (checked: OLPE_EINVAL on every rank otherwise).
+ * folded the same number of rows (checked: OLPE_EINVAL on every rank otherwise); the
+ * walker counts may differ (a sum needs no equal shards).
  * Without olpe_comm_init it summarises this context alone. */
 int olpe_comm_allreduce_moments(olpe_ctx *ctx, double *out);
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "olpe_comm_init": (_i, [_P, _pu8, _i, _i]),
     "olpe_comm_allgather_state": (_i, [_P, _pd]),
     "olpe_comm_allgather_chain": (_i, [_P, _ll, _ll, _pd, _pll]),
+    "olpe_comm_gather_limit": (_i, [_P, _ll]),
     "olpe_comm_allreduce_moments": (_i, [_P, _pd]),
 }
 

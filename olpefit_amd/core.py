@@ -294,6 +294,10 @@ class Sampler:
                                                   C.byref(nrec)))
         return buf
 
+    def gather_limit(self, nbytes: int):
+        """Byte limit of the chain gather's device receive buffer (0 = none)."""
+        check(self._lib.olpe_comm_gather_limit(self._ctx, int(nbytes)))
+
     def allreduce_moments(self):
         """Posterior sums over every rank's walkers (olpe_comm_allreduce_moments; this
         context alone without comm_init): the olpe_moments_summary layout with the

@@ -1319,7 +1319,7 @@ void olpe_destroy(olpe_ctx *c) {
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue,
-                  c->d_gather, c->d_uflag, c->d_mmean, c->d_mm2, c->d_mpart};
+                  c->d_gather, c->d_uflag, c->d_mmean, c->d_mm2, c->d_mpart, c->d_check};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &pair : c->ev)
@@ -1357,14 +1357,19 @@ static int eval_batch(olpe_ctx *c, const double *params, int W, double *out, boo
   const int fast = c->eval_mode == OLPE_EVAL_FAST;
   if (shm > 160 * 1024) return set_err(OLPE_EINVAL, "image too large for the eval kernel");
   if (shm > 65536) {
-    static std::atomic<int> eval_attr{0};
-    if (!eval_attr.exchange(1)) {
+    // per device, like the sampler's (launch_gibbs_t): the device's bit is set only
+    // after every kernel's attribute is, with this context's device current, so a
+    // failed set is retried and no caller launches before it took effect
+    static std::atomic<uint64_t> eval_attr{0};
+    const uint64_t bit = 1ull << (c->device & 63);
+    if (!(eval_attr.load(std::memory_order_acquire) & bit)) {
       const void *ks[4] = {(const void *)olpe_eval_kernel<2, true>,
                            (const void *)olpe_eval_kernel<2, false>,
                            (const void *)olpe_eval_kernel<3, true>,
                            (const void *)olpe_eval_kernel<3, false>};
       for (const void *k : ks)
         HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      eval_attr.fetch_or(bit, std::memory_order_release);
     }
   }
   if (c->nsrc == 2) {

@@ -474,18 +474,22 @@ int olpe_acceptance_write(const char *const *paths, const double *accepts, const
   std::vector<int> failed(nt, -1);
   auto work = [&](unsigned t) {
     std::vector<double> x(np);
-    std::string s;
+    std::string s, tmp;
     for (int i = (int)t; i < nfiles; i += (int)nt) {
       for (int k = 0; k < np; ++k) x[k] = accepts[(size_t)i * np + k] / tries[(size_t)i * np + k];
       done[i] = 0;
       if (!paths[i] || !numpy_str_fixed(x.data(), np, s)) continue;
-      FILE *f = fopen(paths[i], "wb");
+      // a temporary name renamed over the file: a run killed mid-write leaves the
+      // previous complete file, never a truncated one (the checkpoint's acceptance
+      // files are written in the background)
+      tmp.assign(paths[i]).append(".tmp");
+      FILE *f = fopen(tmp.c_str(), "wb");
       if (!f || fwrite(s.data(), 1, s.size(), f) != s.size()) {
         if (f) fclose(f);
         failed[t] = i;
         return;
       }
-      if (fclose(f) != 0) {
+      if (fclose(f) != 0 || rename(tmp.c_str(), paths[i]) != 0) {
         failed[t] = i;
         return;
       }

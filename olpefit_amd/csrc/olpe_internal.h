@@ -76,6 +76,8 @@ struct olpe_ctx {
   int nranks = 1, rank = 0;
   double *d_gather = nullptr;   // receive buffer of olpe_comm_allgather_chain
   size_t gather_cap = 0;
+  size_t gather_limit = 0;      // its byte limit (olpe_comm_gather_limit; 0 = none)
+  long long *d_check = nullptr; // the uniformity check's words (allocated by comm_init)
 };
 
 namespace olpe {

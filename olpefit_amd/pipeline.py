@@ -169,8 +169,13 @@ def acceptance_text(accepts, tries) -> str:
 
 
 def write_acceptance(path: str, accepts, tries) -> None:
-    with open(path, "w") as f:
+    """Write to a temporary name and rename it over the file (as the native writer
+    does), so a run killed mid-write leaves the previous complete file, never a
+    truncated one (the writes run in the background after a checkpoint)."""
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
         f.write(acceptance_text(accepts, tries))
+    os.replace(tmp, path)
 
 
 def write_acceptance_files(paths, accepts, tries, threads: int = 0) -> None:

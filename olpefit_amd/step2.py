@@ -588,12 +588,14 @@ def main(argv=None, nsrc=2, variant="2"):
             with timed("launches (sampler + chain copy)"):
                 hits = np.concatenate([sh.s.done_at() for sh in shards])
             hits = hits[hits >= 0]
-            if hits.size and snaps is None:
-                raise RuntimeError(f"accept_min reached at count {int(hits.min())} before "
-                                   f"{n_par} x {args.accept_min} iterations")
             if group is not None:         # the earliest hit over every rank's walkers
                 first = group.allmax(-float(hits.min()) if hits.size else -np.inf)
                 hits = np.array([int(-first)]) if np.isfinite(first) else hits[:0]
+            # after the reduction, so that every rank raises (`need` is the same on every
+            # rank) instead of one rank leaving its peers in the collective
+            if hits.size and snaps is None:
+                raise RuntimeError(f"accept_min reached at count {int(hits.min())} before "
+                                   f"{n_par} x {args.accept_min} iterations")
             if not hits.size:
                 count += chunk
                 commit()

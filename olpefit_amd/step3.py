@@ -201,6 +201,11 @@ def main(argv=None, nsrc: int = 2):
     additional_burnin = args.additional_burnin or 1                 # :81-84
     _, _, input_directory = pipeline.image_paths(args.image)       # :138-143
     names = NAMES_2 if nsrc == 2 else NAMES_3
+    if args.from_moments and additional_burnin != 1:
+        # the device moments fold every recorded row (additional_burnin = 1): a larger
+        # burn-in cannot be taken out of them afterwards
+        ap.error(f"--from-moments covers every recorded row (additional_burnin 1); "
+                 f"-a {additional_burnin} needs the chain files")
     if args.from_moments:
         with open(input_directory + "posterior_summary.json") as f:
             summ = json.load(f)

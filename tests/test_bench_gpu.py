@@ -42,3 +42,25 @@ def test_bench_default_line_has_posterior_and_profile():
     assert d["posterior"]["walkers"] == 65536 and d["posterior"]["rows_per_walker"] == 30
     r = d["roofline"]
     assert r["frac_source"] == "counters" and 0 < r["frac"] <= 1
+
+
+def test_bench_gpus_flag_two_ranks_share_gpu():
+    """`bench.py --gpus 2` from a plain process (no launcher environment): the parent
+    starts two ranks, makes no HIP call itself, and relays rank 0's line for the two
+    ranks' walkers (on the one-GPU box both share device 0: --share-gpu, no RCCL)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu",
+                        "--walkers", "2048", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-alt"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "walker-sharded x2"
+    assert d["config"]["local_ranks"] == [0, 1] and d["config"]["devices"] == [0, 0]
+    assert d["config"]["launcher"] == "bench.py --gpus"
+    assert d["value"] == pytest.approx(2 * 2048 * 100 * 2 / (d["ms_per_step"] * 2e-3),
+                                       rel=1e-9)
+    assert d["posterior"]["walkers"] == 2 * 2048

@@ -1,0 +1,145 @@
+"""bench.py --gpus N on CPU: the launcher starts N ranks (one process per GPU, distinct
+LOCAL_RANK = device) when no launcher set WORLD_SIZE, relays rank 0's JSON line, and
+reports the N > 1 run as the driver reads it -- with tests/bench_stub.py standing in for
+the per-GPU sampler (no kernel; each launch sleeps a known time).  Reference: the
+launch-sized world of ``mpiexec -n W python apf_step2.py`` (apf_step2.py:27-29, :50-57)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.join(REPO, "tests")
+WPG, ITERS, STRIDE, STEPS = 64, 100, 10, 3
+
+
+def _run(args, extra_env=None, timeout=180):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT",
+                        "TORCHELASTIC_RUN_ID", "OLPE_BENCH_LAUNCHED")}
+    env.update(OLPE_BENCH_SAMPLER="bench_stub:StubSampler", OLPE_STUB_MS="20",
+               PYTHONPATH=os.pathsep.join([TESTS, REPO, env.get("PYTHONPATH", "")]))
+    env.update(extra_env or {})
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--walkers", str(WPG),
+           "--steps", str(STEPS), "--warmup", "1", "--no-cpu-baseline", "--no-alt"] + args
+    return subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def _line(r):
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr)
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_gpus_flag_spawns_n_ranks(n):
+    r = _run(["--gpus", str(n)])
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["n_gpus"] == n
+    c = d["config"]
+    assert c["parallelism"] == f"walker-sharded x{n}"
+    assert c["launcher"] == "bench.py --gpus"
+    assert c["local_ranks"] == list(range(n)) and c["devices"] == list(range(n))
+    # value = every rank's walker-steps / the max-over-ranks wall time of the timed steps
+    total = n * WPG * ITERS * STEPS
+    assert d["value"] == pytest.approx(total / (d["ms_per_step"] * STEPS * 1e-3), rel=1e-9)
+    assert d["ms_per_step"] >= 20.0                        # each stub launch sleeps 20 ms
+    # the exchange: state all-gather checked against this rank's block, then the chain
+    # concatenation over every rank's rows
+    nrec, ps = ITERS // STRIDE, 17
+    assert d["allgather_ms"] is not None and "comm_error" not in d
+    assert d["chain_gather_bytes"] == n * WPG * nrec * ps * 8
+    assert d["chain_gather_ranges"] == 1 and d["chain_gather_range_walkers"] == WPG
+    assert d["chain_gather_gbs"] == pytest.approx(
+        d["chain_gather_bytes"] * (n - 1) / n / (d["chain_gather_ms"] * 1e-3) / 1e9, rel=1e-9)
+    # posterior over every rank's walkers (the all-reduced moments)
+    assert d["posterior"]["walkers"] == n * WPG
+    assert d["posterior"]["rows_per_walker"] == (STEPS + 1) * nrec
+    assert "cpu_baseline" not in d                     # rank 0 at N = 1 only
+
+
+def test_chain_gather_ranges_and_verify():
+    # 64 walkers x 10 rows x 136 B = 87,040 B per rank; a 0.02 MiB range holds 15 walkers
+    r = _run(["--gpus", "2", "--gather-mib", "0.02", "--verify-exchange"])
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    wn = int(0.02 * 2 ** 20 // (10 * 17 * 8))
+    assert d["chain_gather_range_walkers"] == wn
+    assert d["chain_gather_ranges"] == -(-WPG // wn)
+    assert d["exchange_verified"] is True
+
+
+def test_exchange_error_is_reported_in_the_line():
+    r = _run(["--gpus", "2"], {"OLPE_STUB_FAIL": "chain"})
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert "injected failure" in d["comm_error"]
+    assert d["n_gpus"] == 2 and d["value"] > 0            # the measurement survives
+
+
+def test_failed_rank_fails_the_launch():
+    r = _run(["--gpus", "3"], {"OLPE_STUB_FAIL": "rank1"}, timeout=120)
+    assert r.returncode != 0
+    assert "rank 1 exited with status 5" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_world_size_mismatch_is_refused():
+    r = _run(["--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_one_rank_without_launcher():
+    r = _run([])
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["n_gpus"] == 1 and d["config"]["launcher"] == "none (1 rank)"
+    assert d["config"]["devices"] == [0] and d["allgather_ms"] is None
+
+
+def test_config0_line_beside_one_core():
+    """configs[0] (1 walker, 32x32, 1,000 iterations): the GPU's one walker beside the
+    oracle's one walker on one core, and the reference's own rate derived from the
+    build-container ratio (profiles/r04/reference_cpu_timing.json)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
+    env.update(OLPE_BENCH_SAMPLER="bench_stub:StubSampler", OLPE_STUB_MS="5",
+               PYTHONPATH=os.pathsep.join([TESTS, REPO]))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--config", "0",
+                        "--no-alt"], cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    c = d["config"]
+    assert c["walkers_per_gpu"] == 1 and c["image"] == "32x32" and c["iters_per_step"] == 1000
+    assert c["chain_stride"] == 1 and d["steps"] == 1
+    assert d["posterior"]["walkers"] == 1 and d["posterior"]["gr_rc_max"] is None
+    cb = d["cpu_baseline"]
+    assert cb["cores"] == 1 and cb["kind"] == "port" and "1000 iterations" in cb["sample"]
+    assert 0 < cb["reference_over_port"] < 1
+    assert cb["reference_value_derived"] == pytest.approx(cb["value"] * cb["reference_over_port"])
+    assert d["gpu_over_reference"] == pytest.approx(d["value"] / cb["reference_value_derived"])
+
+
+def test_per_config_defaults_cover_the_survey_runs():
+    import bench
+    # configs[0] 1,000 iterations, [1] 10,000 at stride 1, [2] 2,000 at
+    # stride 10, [4] 500 at stride 10
+    tot = {k: v["iters"] * v["steps"] for k, v in bench.DEFAULTS.items()}
+    assert tot == {0: 1000, 1: 10000, 2: 2000, 4: 500}
+    assert [bench.DEFAULTS[k]["stride"] for k in (0, 1, 2, 4)] == [1, 1, 10, 10]
+
+
+def test_share_gpu_ranks_sum_moments_over_the_host_group():
+    r = _run(["--gpus", "3", "--share-gpu"])
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["n_gpus"] == 3 and d["config"]["devices"] == [0, 0, 0]
+    assert d["allgather_ms"] is None                       # no RCCL on a shared GPU
+    p = d["posterior"]
+    assert p["walkers"] == 3 * WPG and p["rows_per_walker"] == (STEPS + 1) * ITERS // STRIDE
+    assert p["means"]["xcs"] == pytest.approx(1.0)

@@ -338,6 +338,17 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
         s.allgather_chain(6, 3)                          # past the last walker
     # the moments all-reduce over the communicator equals the local two-pass summary
     np.testing.assert_array_equal(s.allreduce_moments(), local)
+    # a receive buffer this rank cannot allocate (over the gather limit) is OLPE_ENOMEM,
+    # decided in the same all-reduce as the range check, so every rank returns it
+    # instead of the others entering the gather (verdict r03 item 7)
+    from olpefit_amd._lib import OlpeError
+    s.gather_limit(2048)            # 1 walker x 10 rows x 136 B fits, 8 walkers do not
+    with pytest.raises(OlpeError) as ei:
+        s.allgather_chain()
+    assert ei.value.code == -3 and "receive buffer" in str(ei.value)
+    np.testing.assert_array_equal(s.allgather_chain(0, 1)[0], chain[:1])
+    s.gather_limit(0)
+    np.testing.assert_array_equal(s.allgather_chain()[0], chain)
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
