@@ -83,8 +83,10 @@ struct GibbsArgs {
   unsigned utag;       // this launch's tag base (a multiple of 16)
   unsigned *uerr;      // set to 1 when a hand-off wait times out (olpe_sync reports it)
   unsigned long long wait_ticks;   // a hand-off wait gives up after this many 100 MHz ticks
-  int balance;         // progress balancing of the LDS sampler (OLPE_BALANCE)
-  int stagger;         // start offset per wave rank within a SIMD, in ~0.5 us (OLPE_STAGGER)
+  int balance;         // progress balancing of the LDS sampler (launch_gibbs_t picks)
+  int stagger;         // start offset per wave rank within a SIMD, in ~0.5 us: always 0
+                       // (round 2's OLPE_STAGGER changed nothing; the host knob is gone,
+                       // the argument kept so that the sampler's code is unchanged)
 };
 
 constexpr int kTraceF = 6;
@@ -159,7 +161,7 @@ __host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, in
 // draw tables there (its sweeps park nothing) and the two FAST3 shape-table slots (no
 // V-table fallback)
 template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
-  return WaveSlice<NP>::OPE + kDrawTabBytes + (OLPE_RING_WINDOW ? 1 : 2) * n * 16;
+  return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
 }
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
@@ -254,27 +256,17 @@ __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigne
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-#ifndef OLPE_RING_PRIO_STEP
-// A/B: the ring sampler's sweep priority by wave rank within a SIMD (younger waves ahead
-// of older ones; 0 = the hardware's age order, the default): 2 = priorities 0 / 1 / 2 for
-// waves 0-3 / 4-7 / 8-11 with the ring sampler's control chain at 3.  +0.5-0.8 % on one
-// box (profiles/r03/ab_c4_ring_window.log), +-0.3 % on the next (ab_c4_ring_prio.log)
-#define OLPE_RING_PRIO_STEP 0
-#endif
-#ifndef OLPE_CTRL_PRIO
 // wave priority of the step's control chain (the sweep runs at 0, or 0/1 with balancing)
-#define OLPE_CTRL_PRIO 2
-#endif
-#ifndef OLPE_GLOBAL_WAVES_PER_EU
-#define OLPE_GLOBAL_WAVES_PER_EU 3
-#endif
+constexpr int kCtrlPrio = 2;
+// the global-memory sampler's minimum waves per SIMD (its launch bound, below)
+constexpr int kGlobalWavesPerEU = 3;
 template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // The global-memory (large cutout) variant runs 4-wave workgroups and waits on L2: it
 // is asked to fit 3 of them per CU (168 VGPRs, no spills; 3-source 128x128 +0.9 % over
 // 4 per CU at 128 VGPRs, +4.5 % over 2 per CU)
 // (hipcc passes the second bound on as the minimum waves per SIMD; the ring sampler,
 // NT = 128 with one 12-wave workgroup per CU, keeps 3 per SIMD with 168 VGPRs)
-__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : OLPE_GLOBAL_WAVES_PER_EU)
+__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : kGlobalWavesPerEU)
 void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
@@ -466,12 +458,12 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
-    hcache.single = single_h(NSRC, NT, WPB, FAST) || (RING && OLPE_RING_WINDOW);
+    hcache.single = single_h(NSRC, NT, WPB, FAST);
     GuardCache gcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
     ccache.colc = colc;
-    __builtin_amdgcn_s_setprio(RING && OLPE_RING_PRIO_STEP > 1 ? 3 : OLPE_CTRL_PRIO);
+    __builtin_amdgcn_s_setprio(kCtrlPrio);
 #ifdef OLPE_DIAG_TIMING
     unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long dt_last = __builtin_amdgcn_s_memtime();
@@ -487,13 +479,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       // (:63-70) and accept_reject's rand() (:144), left in drawtab[dice_idx]
       int r0 = 0, dice_idx = 0;
       double g = 0.0;
-#ifdef OLPE_DIAG_NO_GAUSS
-      mt.template draw<NP>(lane, 0, 0, r0, g, dice_idx);
-      mt.template draw<NP>(lane, 2, 2, r0, g, dice_idx);
-      g = 0.01 * (double)(r0 - 8);                  // diagnostic: no polar draw
-#else
       mt.template draw<NP>(lane, 0, 2, r0, g, dice_idx);
-#endif
       const int r = __builtin_amdgcn_readfirstlane(r0);
       // total_tries[rand] += 1  (:304)
       const uint32_t tr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tries[r]) + 1u;
@@ -611,7 +597,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         // +-25 %) and a launch ends on its slowest wave, with the SIMDs under-occupied
         // meanwhile (one full round of walkers took 1.4x the steady-state time).  A wave
         // that has started fewer iterations than its workgroup's mean sweeps at
-        // priority 1, the others at 0 (the control chain runs at OLPE_CTRL_PRIO above
+        // priority 1, the others at 0 (the control chain runs at kCtrlPrio above
         // both).
         const unsigned tot = (unsigned)__builtin_amdgcn_readfirstlane((int)s_prog[0]);
         const bool behind = my_steps * (unsigned)WPB < tot;
@@ -619,13 +605,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         ++my_steps;
         if (behind) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
-      } else if (RING && OLPE_RING_PRIO_STEP) {
-        // A/B (OLPE_RING_PRIO_STEP = d): the ring sampler's lockstep waves sweep at
-        // priority (wave / 4) * d -- younger waves of a SIMD (wave, wave + 4, wave + 8)
-        // ahead of the older ones, against the hardware's age order
-        if ((wave >> 2) == 0) __builtin_amdgcn_s_setprio(0);
-        else if ((wave >> 2) == 1) __builtin_amdgcn_s_setprio(OLPE_RING_PRIO_STEP > 1 ? 1 : 0);
-        else __builtin_amdgcn_s_setprio(OLPE_RING_PRIO_STEP > 1 ? 2 : 1);
       } else {
         __builtin_amdgcn_s_setprio(0);
       }
@@ -651,7 +630,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
                                                      &hcache, &ccache, gmask, &gcache,
                                                      RING ? &ring : nullptr);
       }
-      __builtin_amdgcn_s_setprio(RING && OLPE_RING_PRIO_STEP > 1 ? 3 : OLPE_CTRL_PRIO);
+      __builtin_amdgcn_s_setprio(kCtrlPrio);
       DT_MARK(3);
       // (the total is valid in lane 63: the accept ballots that lane's test, and lane 63
       // stores an accepted chi^2, so the step needs no readlanes of the sum)
@@ -684,9 +663,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       hcache.after(acc);
       gcache.after(acc);
       if constexpr (FAST && NT != 0 && NT <= 64) {
-#ifndef OLPE_DIAG_NO_REFRESH
         if (acc && gmask) colcache_accept<NSRC, NT>(ccache, *mdl, gmask, lane, etab);
-#endif
         ccache.pend = 0;              // parked terms belong to this step only
       }
       wave_sync();
@@ -1288,7 +1265,6 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     }
     c->units_override = p;
   }
-  if (const char *e = getenv("OLPE_BALANCE")) c->balance = atoi(e) != 0;   // A/B
   if (const char *e = getenv("OLPE_RING")) {                                // A/B, tests
     const int v = atoi(e);
     if (v != 0 && v != 12) {
@@ -1297,7 +1273,6 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
     }
     c->ring_wpb = v;
   }
-  if (const char *e = getenv("OLPE_STAGGER")) c->stagger = std::max(0, std::min(1000, atoi(e)));
   // tests only: the hand-off wait limit in 100 MHz ticks instead of the launch's bound
   if (const char *e = getenv("OLPE_WAIT_TICKS")) c->wait_ticks_override = std::max(0.0, atof(e));
   hipError_t e2 = hipMemcpy(c->d_DE, hDE.data(), npix * sizeof(double2), hipMemcpyHostToDevice);

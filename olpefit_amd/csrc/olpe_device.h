@@ -103,38 +103,16 @@ __device__ __forceinline__ double lane63_f64(double v) {
 }
 __device__ __forceinline__ double wave_sum_dpp(double v) { return lane63_f64(wave_sum_dpp_v(v)); }
 
-// The same sum on the matrix core: two v_mfma_f64_16x16x4_f64 against a ones matrix.
-// The first takes lane l as A[l & 15][l >> 4] and leaves s_i = sum of lanes i, i+16,
-// i+32, i+48 in rows i of D, lane l holding rows (l >> 4) + 4r in its four result
-// registers (r = 0..3); three adds fold r, so lane l holds t_(l >> 4), and the second
-// MFMA sums the four t over its k dimension into every lane.  8 VALU-port instructions
-// (the ones constant, 2 MFMA, 3 adds, 2 lane reads) where the DPP tree issues 20; the
-// MFMAs run on the matrix core (the sampler does no other matrix work).  Measured 1.5 %
-// slower than the DPP tree on configs[2] (profiles/r02/ab_wavesum_mfma.log): not the
-// default.  A NaN partial propagates (a NaN chi^2 rejects).
-typedef double olpe_v4f64 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ double wave_sum_mfma(double v) {
-  const olpe_v4f64 z = {0.0, 0.0, 0.0, 0.0};
-  const olpe_v4f64 d = __builtin_amdgcn_mfma_f64_16x16x4f64(v, 1.0, z, 0, 0, 0);
-  const double t = (d[0] + d[1]) + (d[2] + d[3]);
-  const olpe_v4f64 e = __builtin_amdgcn_mfma_f64_16x16x4f64(t, 1.0, z, 0, 0, 0);
-  return uniform_f64(e[0]);
-}
-
+// (The same sum on the matrix core -- two v_mfma_f64_16x16x4_f64 against a ones matrix,
+// 8 VALU-port instructions where the DPP tree issues 20 -- ran 1.5 % slower on
+// configs[2]: an FP64 MFMA holds the FP64 pipe; profiles/r02/ab_wavesum_mfma.log, removed
+// in round 4.)
 __device__ __forceinline__ double wave_sum(double v) {
-#ifdef OLPE_WAVESUM_MFMA
-  return wave_sum_mfma(v);       // A/B builds: 1.5 % slower on configs[2]
-#else
   return wave_sum_dpp(v);
-#endif
 }
-// the wave sum valid in lane 63 (every lane for the MFMA form)
+// the wave sum valid in lane 63
 __device__ __forceinline__ double wave_sum_v(double v) {
-#ifdef OLPE_WAVESUM_MFMA
-  return wave_sum_mfma(v);
-#else
   return wave_sum_dpp_v(v);
-#endif
 }
 
 // ---------------------------------------------------------------------------------
@@ -1320,7 +1298,6 @@ __device__ __forceinline__ void moved_terms(MovedTerms<NSRC> &mt, const ModelDes
     mt.gi[k] = rest ? __builtin_ctz(rest) : -1;
     rest &= rest - 1u;
   }
-#ifndef OLPE_DIAG_NO_COLTERM
   if (mt.nm >= 2) {
     // (two moved with three sources: the third term repeats the first one)
 #pragma unroll
@@ -1335,7 +1312,6 @@ __device__ __forceinline__ void moved_terms(MovedTerms<NSRC> &mt, const ModelDes
       mt.R[k] = t.R;
     }
   }
-#endif
 }
 
 template <int NSRC, int NT, bool WRITE, bool CC = false, bool WIDE = false>
@@ -1361,7 +1337,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     double av[G], rho[G];
     // the moved Gaussians' terms come precomputed (moved_terms, before the guard)
     if constexpr (CC) {
-#ifndef OLPE_DIAG_NO_COLTERM
       if (pre->nm >= 2) {
 #ifdef OLPE_DIAG_TIMING
         cc->n_setup += pre->nm;
@@ -1376,16 +1351,12 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           }
         }
       }
-#endif
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       ColTerm t;
       if constexpr (CC) {
         const bool mine = (gmask >> g) & 1u;
-#ifdef OLPE_DIAG_NO_COLTERM
-        if (true) {                              // diagnostic: column terms never recomputed
-#else
         if (mine) {
           double e = pre->E[0], r = pre->R[0];
 #pragma unroll
@@ -1395,7 +1366,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           }
           t = ColTerm{e, r};
         } else if ((cc->valid >> g) & 1u) {
-#endif
           t = ColTerm{cc->E[g], cc->R[g]};
         } else {                 // (first step of a walker) a term of the current state
           if constexpr (NT == 64)
@@ -1459,16 +1429,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // was +1.0-1.4 % over the 12-wave sampler; the two-row update ran level with 12
     // waves (profiles/r02/ab_w16.log)
     constexpr bool LEAN = NSRC == 3 && (NT == 64 || NT == 32);
-#ifdef OLPE_ROWU
-    constexpr int RU = OLPE_ROWU;      // rows per update (2 or 4): A/B builds
-#else
     constexpr int RU = LEAN ? 2 : 4;
-#endif
-#ifdef OLPE_H_PREFETCH
-    constexpr bool HPF = OLPE_H_PREFETCH;
-#else
     constexpr bool HPF = !LEAN;
-#endif
     double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -1550,16 +1512,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
           voff = (cw.grp * n + jj) * 16;
         }
         auto img = [&](int r) -> double2 {
-#if defined(OLPE_DIAG_IMG_ROWS)
-          // diagnostic build only: every cutout read from the first OLPE_DIAG_IMG_ROWS
-          // rows (L1-resident), results meaningless -- what the L2-resident sampler loses
-          // to its cutout reads
-          r &= OLPE_DIAG_IMG_ROWS - 1;
-#endif
-#if defined(OLPE_DIAG_IMG_NONE)
-          // diagnostic build only: no cutout reads at all (per-row constants)
-          return make_double2(1e-3 * (double)r, 1.0 / 38.0);
-#endif
           if constexpr (NT > 64) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, r * rstep * 16, 0);
             double2 d;
@@ -1627,31 +1579,14 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // The DMA is issued from inline asm: the compiler then inserts no vmcnt(0) before the
 // issuing wave's next LDS reads (it cannot tell the ring slots apart), and its own
 // counted waits stay correct because vector memory operations retire in order.
-//
-// Windowed form (OLPE_RING_WINDOW, round 3): five slots of 16-row phases, the DMA of
-// phase g + 3 issued at the start of phase g, and no s_barrier per phase: a wave that
-// starts phase g first waits for its LDS reads and for its DMA shares but the latest
-// phase's (so it no longer reads phase g - 1 and its share of phase g + 1 has landed),
-// counts itself in with an LDS atomic (arrive[g % 5]), and then waits only until every
-// wave has started phase g - 1 -- which is when phase g's DMA has landed everywhere and
-// the slot of phase g + 3 (phase g - 2's) is read by nobody.  The waves of a workgroup
-// may so drift one phase apart (the oldest wave of a SIMD runs into the next phase while
-// the younger ones finish, instead of idling at a barrier), and each DMA has two phases
-// to land.  (The first form, four slots with the DMA two phases ahead and every DMA
-// drained at the next phase, stalled on its own loads: 6 % slower.)  Its 80 KiB of ring
-// fit beside 12 wave slices with one shape-table slot per wave (HCache::single).
-#ifndef OLPE_RING_WINDOW
-#define OLPE_RING_WINDOW 0
-#endif
+
+// (Windowed rings without barriers -- four and five slots of 16-row phases -- ran 6 %
+// and 9 % slower; DESIGN.md §7.2, removed in round 4.)
 template <int WAVES> struct LdsRing {
-#if OLPE_RING_WINDOW
-  static constexpr int ROWS = 16, SLOTS = 5, AHEAD = 3;
-#else
   static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
   static constexpr int SLOTS = 2, AHEAD = 1;              // ring slots; DMA lead in phases
-#endif
   static constexpr int SLOT = ROWS * 64 * 16;
-  static constexpr int BYTES = SLOTS * SLOT + (OLPE_RING_WINDOW ? 64 : 0);   // + counters
+  static constexpr int BYTES = SLOTS * SLOT;
   static constexpr int PPP = 128 / ROWS;                  // phases per column pass
   static constexpr int PHASES = 2 * PPP;                  // phases per 128x128 sweep
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
@@ -1662,10 +1597,6 @@ template <int WAVES> struct LdsRing {
   unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
-#if OLPE_RING_WINDOW
-  unsigned *arrive;      // windowed form: [SLOTS] arrival counters after the slots
-  int nshare;            // DMA instructions of this wave per phase (its rows of the phase)
-#endif
 #ifdef OLPE_DIAG_TIMING
   // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
   // phase of a step (behind the workgroup's slowest control section) and at the others
@@ -1694,9 +1625,8 @@ template <int WAVES> struct LdsRing {
     for (int rr = 0; rr < ROWS; rr += WAVES)
       if (rr + wave < ROWS) dma_row(ph, sl, rr + wave);
   }
-  // before the first phase: phases 0 .. AHEAD-1 into their slots (the windowed form
-  // zeroes its counters too; the workgroup barrier of the first take_batch orders both
-  // before any wave's first phase)
+  // before the first phase: phase 0 into slot 0 (the workgroup barrier of the first
+  // take_batch orders it before any wave's first phase)
   __device__ __forceinline__ void prologue(unsigned char *ring_lds, const double2 *dw, int w,
                                            int lane) {
     base = reinterpret_cast<const double2 *>(ring_lds);
@@ -1705,68 +1635,10 @@ template <int WAVES> struct LdsRing {
     wave = w;
     voff = (unsigned)lane * 16u;
     g = 0;
-#if OLPE_RING_WINDOW
-    arrive = reinterpret_cast<unsigned *>(ring_lds + SLOTS * SLOT);
-    nshare = w < ROWS ? (ROWS - 1 - w) / WAVES + 1 : 0;
-    if (w == 0 && lane < SLOTS) arrive[lane] = 0u;
-#pragma unroll
-    for (int p = 0; p < AHEAD; ++p) dma_phase(p, p % SLOTS);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
     dma_phase(0, 0);
-#endif
   }
-#if OLPE_RING_WINDOW
-  // opens phase g (windowed form, above); returns phase g's slot
-  __device__ __forceinline__ const double2 *begin_phase() {
-#ifdef OLPE_DIAG_TIMING
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-    // this wave's LDS reads done, and its DMA shares landed up to phase g + AHEAD - 2:
-    // only the latest phase's (issued at the previous begin_phase) may stay in flight, so
-    // the arrival below certifies this wave's share of phase g + 1 -- two phases after
-    // it was issued.  Vector memory operations retire in order.  At a step's first phase
-    // the step's control section (key loads, chain stores) sits after the latest DMA, so
-    // the wait there is for everything (more than needed, never less).
-    if (g % PHASES == 0 || g < (unsigned)AHEAD || nshare <= 0 || nshare > 2)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else if (nshare == 1)
-      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-    typedef __attribute__((address_space(3))) unsigned lds_u32;
-    lds_u32 *cnt = (lds_u32 *)arrive;
-    if (voff == 0) __hip_atomic_fetch_add(cnt + g % SLOTS, 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (g > 0) {
-      const unsigned p = g - 1;
-      const unsigned want = (unsigned)WAVES * (p / SLOTS + 1u);
-      for (;;) {
-        const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
-            cnt + p % SLOTS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if ((int)(v - want) >= 0) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    asm volatile("" ::: "memory");
-#ifdef OLPE_DIAG_TIMING
-    const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t0;
-    if (g % PHASES == 0) wait_first += dtw;
-    else wait_rest += dtw;
-#endif
-    dma_phase((int)((g + AHEAD) % PHASES), (int)((g + AHEAD) % SLOTS));
-    const double2 *ph = base + (g % SLOTS) * (SLOT / 16);
-    ++g;
-    return ph;
-  }
-#else
   // the barrier that opens phase g; returns phase g's slot
   __device__ __forceinline__ const double2 *begin_phase() {
-#ifdef OLPE_DIAG_NO_BARRIER
-    // diagnostic build only: no barrier (the ring races, results meaningless) -- what
-    // the lockstep costs
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#else
 #ifdef OLPE_DIAG_TIMING
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1776,13 +1648,11 @@ template <int WAVES> struct LdsRing {
     if (g % PHASES == 0) wait_first += dtw;
     else wait_rest += dtw;
 #endif
-#endif
     dma_phase((int)((g + 1) % PHASES), (int)((g + 1) & 1));
     const double2 *p = base + (g & 1) * (SLOT / 16);
     ++g;
     return p;
   }
-#endif
   // a step without a sweep of this wave's own (idle wave, or a fallback sweep that read
   // the cutout from global memory): the phases' barriers and DMA shares only
   __device__ __forceinline__ void idle_step() {
@@ -1931,14 +1801,6 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
                                         ColCache<2 * NSRC> *cc = nullptr, unsigned gmask = 0,
                                         GuardCache *gc = nullptr, RingT *ring = nullptr) {
   // img is {D, 1/err} for EXACT kernels and {D/err, 1/err} for FAST kernels
-#ifdef OLPE_DIAG_NO_SWEEP
-  // diagnostic build only (tools/diag_build.sh): the sweep replaced by one LDS read so
-  // the remaining per-step cost can be timed; results are meaningless
-  if constexpr (!WRITE) {
-    asm volatile("" ::"v"(m.g[0].amp), "v"(m.bg));
-    return img[lane].x * 1e-300;
-  }
-#endif
   if constexpr (FAST) {
     const int nn = NT ? NT : n;
     const ColWalk cw(nn, lane);
@@ -1950,9 +1812,6 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
     MovedTerms<NSRC> pre;
     if constexpr (NT != 0 && NT <= 64)
       moved_terms<NSRC, NT>(pre, m, gmask, nn, lane, kc, ExpTab{etab}, cc->colc);
-#ifdef OLPE_DIAG_NO_GUARD
-    const bool ok3 = true;                       // diagnostic: guard skipped
-#else
     bool ok3;
     // the per-column guard only where the whole-grid one can fail on a well-placed
     // model (cutouts wider than 64 columns), and only for the Gaussians that failed
@@ -1983,7 +1842,6 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       else ok3 = fast3_ok<NSRC>(m, nn, rows0, kc, lane);
       if (gc) gc->prop = ok3;
     }
-#endif
     asm volatile("" ::: "memory");
 #ifdef OLPE_DIAG_FALLBACK
     if (!WRITE && lane == 0) atomicAdd(&g_diag_fb[ok3 ? 0 : (fast_level<NSRC>(m, nn) == 2 ? 1 : fast_level<NSRC>(m, nn) == 1 ? 2 : 3)], 1ull);

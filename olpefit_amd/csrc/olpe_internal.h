@@ -58,10 +58,10 @@ struct olpe_ctx {
   bool units_used = false;  // some launch handed chunks between waves (check_units)
   double wait_limit_s = 30; // hand-off wait limit of the last launch (unit_wait)
   double wait_ticks_override = 0;  // OLPE_WAIT_TICKS (tests of the time-out path)
-  int balance = -1;         // progress balancing (OLPE_BALANCE 0/1; -1: launch_gibbs_t picks)
+  int balance = -1;         // progress balancing (-1: launch_gibbs_t picks)
   int ring_wpb = 12;        // 128x128 FAST: the lockstep LDS-ring sampler's waves per
                             // workgroup, 0 = the L2-resident sampler (OLPE_RING)
-  int stagger = 0;          // wave start offsets (OLPE_STAGGER)
+  int stagger = 0;          // wave start offsets (always 0; see GibbsArgs)
   // whole-run moments of the recorded rows (olpe_moments.hip): running mean / M2 per
   // walker and column, [ps][W]; mom_n rows folded per walker; mom_folded = the launch
   // whose rows were folded last (a launch is folded at most once)

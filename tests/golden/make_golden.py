@@ -232,6 +232,42 @@ def make_case(name, n, nsrc, n_walkers, accept_min, burn_in, n_model=None, nonfi
     print(name, "iterations per walker:", lens, "chi2[0]:", chis[0])
 
 
+def make_long_case(name, n, nsrc, n_walkers, accept_min, burn_in):
+    """Round 4: long reference-executed chains, for posterior-level parity against the
+    reference's own lines (not only the oracle).  The same harness as make_case, run
+    to a larger accept_min; only the parameter rows (the state after every iteration,
+    what the chain files hold past burn-in) and the accept flags are stored."""
+    spec = TWO if nsrc == 2 else THREE
+    image, _ = synth.make_image(n, nsrc, seed=0)
+    image = image.astype(">f4")
+    header = dict((k.lower(), v) for k, v in synth.HEADER.items())
+    guess = synth.guess_values(n, nsrc)
+    seeds = np.arange(1000, 1000 + n_walkers)
+    rows, accs, p0 = [], [], None
+    with tempfile.TemporaryDirectory() as td:
+        for w, s in enumerate(seeds):
+            # burn_in past the run: the reference's O(n^2) stacking and rewrite of the
+            # chain file is skipped (the rows come from the trace), not its sampling
+            tr, p0, _ = run_reference_loop(spec, image, header, guess, int(s), accept_min,
+                                           10 ** 9, td, w)
+            rows.append(np.array([t[5] for t in tr]))
+            accs.append(np.array([t[4] for t in tr]))
+            print(name, "walker", w, "iterations", len(tr), flush=True)
+    lens = np.array([len(r) for r in rows])
+    L = lens.max()
+    P = len(p0)
+    t_par = np.full((n_walkers, L, P), np.nan)
+    t_acc = np.zeros((n_walkers, L), bool)
+    for w in range(n_walkers):
+        t_par[w, :lens[w]] = rows[w]
+        t_acc[w, :lens[w]] = accs[w]
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), image=np.asarray(image, np.float32),
+                        guess=np.array(guess), p_init=p0, seeds=seeds, traj_len=lens,
+                        traj_params=t_par, traj_acc=t_acc, accept_min=np.int64(accept_min),
+                        nsrc=np.int64(nsrc))
+    print(name, "iterations per walker:", list(lens))
+
+
 def make_rng():
     seeds = [0, 1, 5489, 12345, 2 ** 32 - 1] + list(range(1000, 1008))
     raw, gauss, unif, ri16, ri19 = [], [], [], [], []
@@ -275,6 +311,12 @@ def make_fits():
 
 if __name__ == "__main__":
     np.seterr(all="ignore")
+    if sys.argv[1:] == ["long"]:
+        # round 4: >= 5,000 iterations x 4 walkers (64x64, 2 sources) and >= 1,500 x 2
+        # (128x128, 3 sources) from the reference's own loop
+        make_long_case("c64_long", 64, 2, n_walkers=4, accept_min=340, burn_in=0)
+        make_long_case("c128_3_long", 128, 3, n_walkers=2, accept_min=90, burn_in=0)
+        sys.exit(0)
     if sys.argv[1:] == ["nonfinite"]:
         # round 3: cutouts with NaN / -inf / +inf data pixels (the reference's np.ma
         # chi_squared drops them, apf_step2.py:134-137 on the array from :188)

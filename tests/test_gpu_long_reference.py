@@ -1,0 +1,63 @@
+"""Long runs against the reference's OWN loop, not only the oracle (round 4).
+
+tests/golden/make_golden.py ``long`` executed apf_step2.py:298-338 (3body :324-373)
+with astropy 4.3.1 to accept_min 340 (4 walkers, 64x64, 2 sources: ~5,900 iterations
+each) and 90 (2 walkers, 128x128, 3 sources: ~1,900 each), and stored the state after
+every iteration.  The HIP sampler, from the same start and seeds, must give every row
+(FAST and EXACT, the trajectory tolerances of test_gpu_parity.py) and the same accept
+decisions; then the posterior statistics step 3 computes (apf_step3.py:258-278: mean,
+sigma, Gelman-Rubin RC) over the HIP chains must equal those over the reference's
+chains, and the source centroids must agree within the north star's 1e-3 px (the
+difference is printed).
+"""
+import numpy as np
+import pytest
+
+from olpefit_amd import step3
+
+pytestmark = pytest.mark.gpu
+TRAJ = {"exact": 1e-10, "fast": 1e-9}
+
+
+def _run(g, mode):
+    from olpefit_amd.core import Sampler
+    nsrc = int(g["nsrc"])
+    s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=nsrc)
+    s.set_eval_mode(mode)
+    seeds = g["seeds"]
+    s.seed(seeds)
+    s.set_state(np.tile(g["p_init"], (len(seeds), 1)))
+    L = int(g["traj_len"].min())
+    s.enable_trace(True)
+    chain = s.run(L, burn_in=0, record_stride=1)
+    tr = s.trace(L)
+    s.close()
+    return chain, tr, L
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+@pytest.mark.parametrize("name", ["c64_long", "c128_3_long"])
+def test_long_chains_match_the_reference(golden, name, mode):
+    g = golden(name)
+    nsrc = int(g["nsrc"])
+    chain, tr, L = _run(g, mode)
+    ref = g["traj_params"][:, :L]
+    assert L >= (5000 if nsrc == 2 else 1500)
+    for w in range(len(g["seeds"])):
+        np.testing.assert_array_equal(tr[w, :, 5] != 0, g["traj_acc"][w, :L],
+                                      err_msg=f"{name} walker {w}: accept decisions")
+        np.testing.assert_allclose(chain[w], ref[w], rtol=TRAJ[mode],
+                                   err_msg=f"{name} walker {w}")
+    # step 3's statistics over both ensembles ([rows, walkers, PS], every row)
+    ours = step3.summary(np.transpose(chain, (1, 0, 2)), nsrc)
+    theirs = step3.summary(np.transpose(ref, (1, 0, 2)), nsrc)
+    names = step3.NAMES_2 if nsrc == 2 else step3.NAMES_3
+    for k in names[:-1]:
+        for stat in ("mean", "median", "std", "gr_rc"):
+            assert ours[k][stat] == pytest.approx(theirs[k][stat], rel=1e-9, abs=1e-12), \
+                (name, k, stat)
+    cen = names[:2 * nsrc]                     # xcs, ycs, xcc, ycc (, xc3, yc3)
+    dpx = max(abs(ours[k]["mean"] - theirs[k]["mean"]) for k in cen)
+    print(f"{name} {mode}: {L} iterations x {len(g['seeds'])} walkers, max centroid "
+          f"difference to the reference {dpx:.3e} px")
+    assert dpx <= 1e-3

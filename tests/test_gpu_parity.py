@@ -413,7 +413,7 @@ def test_configs1_default_launch_matches_oracle(lib_loaded, monkeypatch):
     from olpefit_amd import synth
     from olpefit_amd.core import Sampler
     from olpefit_amd.pipeline import initial_parameters
-    for k in ("OLPE_UNITS", "OLPE_NO_QUEUE", "OLPE_BALANCE", "OLPE_WPB", "OLPE_STAGGER"):
+    for k in ("OLPE_UNITS", "OLPE_NO_QUEUE", "OLPE_WPB", "OLPE_RING"):
         monkeypatch.delenv(k, raising=False)
     n, W = 64, 4096
     img, _ = synth.make_image(n, 2, 0)
@@ -436,6 +436,45 @@ def test_configs1_default_launch_matches_oracle(lib_loaded, monkeypatch):
     st, tries, acc = s.get_state()
     assert np.all(tries.sum(axis=1) == 200) and np.all(acc <= tries)
     assert np.array_equal(st, chain[:, -1, :])
+
+
+def test_configs1_survey_shape_matches_oracle(lib_loaded, monkeypatch):
+    """configs[1] as SURVEY.md 8(d) specifies it and bench.py --config 1 now runs it:
+    4,096 walkers, 1,000-iteration launches with the chain recorded every iteration
+    (apf_step2.py:342-351) and each launch folded into the device moments.  Two
+    launches: sampled walkers equal the oracle row for row over all 2,000 iterations, and
+    every walker's device (mean, M2) equals NumPy's over its 2,000 rows."""
+    from olpefit_amd import synth
+    from olpefit_amd.core import Sampler
+    from olpefit_amd.pipeline import initial_parameters
+    for k in ("OLPE_UNITS", "OLPE_NO_QUEUE", "OLPE_WPB", "OLPE_RING"):
+        monkeypatch.delenv(k, raising=False)
+    n, W = 64, 4096
+    img, _ = synth.make_image(n, 2, 0)
+    dm, err, _, _ = ora.noise_model(img, 1.0, 1, 1, 2)
+    p0 = initial_parameters(img, synth.guess_values(n, 2), 2)
+    s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+    p0[-1] = s.chi_squared(p0)
+    seeds = 1000 + np.arange(W)
+    s.seed(seeds)
+    s.set_state(np.tile(p0, (W, 1)))
+    parts = []
+    for _ in range(2):
+        parts.append(s.run(1000, burn_in=0, record_stride=1))
+        s.moments_accumulate()
+    chain = np.concatenate(parts, axis=1)
+    assert chain.shape == (W, 2000, s.ps) and np.all(np.isfinite(chain))
+    for w in (0, 1, W // 2 + 255, W - 1):
+        ref, _ = ora.Walker(dm, err, p0, int(seeds[w])).run(2000, record_stride=1)
+        np.testing.assert_allclose(chain[w], ref, rtol=10 * TOL["fast"]["traj"], atol=1e-9,
+                                   err_msg=f"walker {w}")
+    nrow, mean, m2 = s.moments()
+    assert nrow == 2000
+    np.testing.assert_allclose(mean, chain.mean(axis=1), rtol=1e-12, atol=1e-12)
+    dev = chain - chain.mean(axis=1, keepdims=True)
+    np.testing.assert_allclose(m2, (dev * dev).sum(axis=1), rtol=1e-8, atol=1e-12)
+    st, tries, acc = s.get_state()
+    assert np.all(tries.sum(axis=1) == 2000) and np.array_equal(st, chain[:, -1, :])
 
 
 def test_bench_3source_128_matches_oracle(lib_loaded):

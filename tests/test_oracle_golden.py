@@ -122,3 +122,17 @@ def test_nonfinite_pixels_drop_out(golden, name):
         chi = np.sum(((img.astype(np.float64)[keep] - m[keep]) / err[keep]) ** 2)
         assert np.isfinite(g["chi2"][k])
         np.testing.assert_allclose(chi, g["chi2"][k], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name,walker", [("c64_long", 3), ("c128_3_long", 1)])
+def test_oracle_long_chain_matches_reference(golden, name, walker):
+    """The round-4 long fixtures (make_golden.py ``long``: the reference's own loop to
+    accept_min 340 / 90): one walker's whole chain (5,775 / 1,945 iterations) from the
+    oracle equals the reference's row for row."""
+    g = golden(name)
+    nsrc = int(g["nsrc"])
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    L = int(g["traj_len"][walker])
+    w = ora.Walker(dm, err, g["p_init"], int(g["seeds"][walker]), nsrc)
+    chain, _ = w.run(L)
+    np.testing.assert_allclose(chain, g["traj_params"][walker, :L], rtol=1e-12, atol=0)

@@ -11,14 +11,15 @@
 # recomputable from the committed files.
 #   tools/roofline_session.sh <tag> [keys...]    (keys: fast exact c1_fast c4_fast)
 export TMPDIR=/tmp
-tag=${1:-r03}; shift
+tag=${1:-r04}; shift
 keys=${*:-"fast exact c1_fast c4_fast"}
 for key in $keys; do
   case $key in
-    fast) cfg=2; mode=fast; steps=10; warm=2;;
+    # (round 4: each config's bench defaults -- SURVEY 8(d)'s iterations and stride)
+    fast) cfg=2; mode=fast; steps=20; warm=5;;
     exact) cfg=2; mode=exact; steps=4; warm=1;;
-    c1_fast) cfg=1; mode=fast; steps=200; warm=50;;
-    c4_fast) cfg=4; mode=fast; steps=10; warm=2;;
+    c1_fast) cfg=1; mode=fast; steps=10; warm=2;;
+    c4_fast) cfg=4; mode=fast; steps=5; warm=2;;
     *) echo "unknown key $key"; exit 2;;
   esac
   B="python bench.py --config $cfg --mode $mode --no-cpu-baseline --no-alt"
