@@ -163,13 +163,13 @@ int olpe_comm_allgather_chain(olpe_ctx *c, long long w0, long long wn, double *o
   const size_t need = per * c->nranks;
   bool alloc_failed = false;
   hipError_t ae = hipSuccess;
-  if (need > c->gather_cap) {
+  if (c->gather_limit && need * sizeof(double) > c->gather_limit) {
+    alloc_failed = true;                                // olpe_comm_gather_limit
+  } else if (need > c->gather_cap) {
     if (c->d_gather) (void)hipFree(c->d_gather);
     c->d_gather = nullptr;
     c->gather_cap = 0;
-    if (c->gather_limit && need * sizeof(double) > c->gather_limit)
-      alloc_failed = true;                              // olpe_comm_gather_limit
-    else if ((ae = hipMalloc(&c->d_gather, need * sizeof(double))) != hipSuccess) {
+    if ((ae = hipMalloc(&c->d_gather, need * sizeof(double))) != hipSuccess) {
       c->d_gather = nullptr;
       alloc_failed = true;
     } else {
