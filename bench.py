@@ -501,6 +501,12 @@ def main():
                     # line's frac differs from it by this box's speed (kernel_ms ratio)
                     out["profile"] = dict(prof, frac_ratio_live_over_profile=(
                         prof["rocprof_kernel_ms"] / kernel_ms))
+                    if prof.get("clock_ghz"):
+                        # the chip holds ~2.0-2.26 GHz under this FP64 load, not the 2.4 GHz
+                        # of the peak (MI355X_MICROARCH.md 'DVFS give-back'): the session's
+                        # fraction of the FP64 issue rate at the clock it held
+                        out["profile"]["frac_of_held_clock_peak"] = (
+                            prof["frac"] * 2.4 / prof["clock_ghz"])
             else:                       # no counters for this shape: the model's own count
                 ops = work_per_step(n, nsrc, mode)
                 out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
@@ -546,7 +552,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
-            "config": {"workload": CONFIG_NAMES[args.config], "walkers_per_gpu": wpg,
+            "config": {"workload": (CONFIG_NAMES[args.config] if not (
+                           args.config == 2 and world == 8 and wpg == 65536) else
+                           "configs[3]: 524,288 walkers sharded 8 x MI355X (65,536 per GPU, "
+                           "64x64 2-source cutout, fp64), RCCL chain all-gather at the end"),
+                       "walkers_per_gpu": wpg,
                        "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                        "chain_stride": args.stride, "eval": args.mode,
                        "chunks_per_walker": units,

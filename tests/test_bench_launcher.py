@@ -143,3 +143,12 @@ def test_share_gpu_ranks_sum_moments_over_the_host_group():
     p = d["posterior"]
     assert p["walkers"] == 3 * WPG and p["rows_per_walker"] == (STEPS + 1) * ITERS // STRIDE
     assert p["means"]["xcs"] == pytest.approx(1.0)
+
+
+def test_eight_ranks_name_configs3():
+    """--gpus 8 at configs[2]'s 65,536 walkers per GPU is SURVEY 8(d)'s configs[3]."""
+    r = _run(["--gpus", "8", "--walkers", "65536", "--steps", "1"], {"OLPE_STUB_MS": "2"})
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["config"]["workload"].startswith("configs[3]: 524,288 walkers")
+    assert d["posterior"]["walkers"] == 524288
