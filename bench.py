@@ -409,10 +409,22 @@ def main():
         wpg = args.walkers
     img, _ = synth.make_image(n, nsrc, 0)
     shared = args.share_gpu or args.share_gpu_rccl
-    device = 0 if shared else local
+    device = 0 if shared else odist.rank_device(local, Sampler.device_count())
     s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc, device=device)
-    # which process / device each rank is (the line names them: one process per GPU)
-    placement = group.allgather([rank, local, device, os.getpid()])
+    # which process / device each rank is (the line names them: one process per GPU);
+    # the PCI bus ids tell whether the ranks really hold distinct GPUs, whatever each
+    # process sees as its device 0..n-1
+    placement = group.allgather([rank, local, device, os.getpid(),
+                                 Sampler.device_pci_id(device)])
+    pci = [p[4] for p in placement]
+    if world > 1 and not shared and len(set(pci)) < world:
+        # the same verdict on every rank (the gathered list is the same everywhere)
+        print(f"[bench rank {rank}] ranks share a GPU (PCI {pci}): one process per GPU "
+              "needs as many GPUs as ranks (--share-gpu for a rehearsal on fewer)",
+              file=sys.stderr)
+        s.close()
+        group.close()
+        sys.exit(4)
     # step-1 style start (apf_step2.py:264-289) for every walker
     from olpefit_amd.pipeline import initial_parameters
     p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
@@ -562,6 +574,7 @@ def main():
                        "chunks_per_walker": units,
                        "parallelism": f"walker-sharded x{world}",
                        "devices": [p[2] for p in placement],
+                       "pci_bus_ids": sorted(set(pci)),
                        "local_ranks": [p[1] for p in placement],
                        "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
                                     else "environment" if "WORLD_SIZE" in os.environ

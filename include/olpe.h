@@ -52,6 +52,10 @@ int olpe_device_count(int *count);
 /* Free / total device memory of a HIP device (sizes a run's launches so that the
  * per-launch chain buffer fits; OLPE_EHIP without a GPU). */
 int olpe_device_mem(int device, long long *free_bytes, long long *total_bytes);
+/* PCI bus id ("dddd:bb:dd.f") of a HIP device into buf (len >= 16): a multi-process run
+ * checks that its ranks' devices are distinct GPUs whatever each process sees as device
+ * 0..n-1 (bench.py, one process per GPU).  Build-specific: no reference counterpart. */
+int olpe_device_pci_id(int device, char *buf, int len);
 /* Thread-local message describing the last error. */
 const char *olpe_last_error(void);
 

@@ -37,6 +37,7 @@ SIGNATURES = {
     "olpe_version": (_i, []),
     "olpe_device_count": (_i, [C.POINTER(_i)]),
     "olpe_device_mem": (_i, [_i, _pll, _pll]),
+    "olpe_device_pci_id": (_i, [_i, C.c_char_p, _i]),
     "olpe_last_error": (C.c_char_p, []),
     "olpe_create": (_i, [_P, _i, _P, _d, _pu8, _i, _i, _i, _i, _i, C.POINTER(_P)]),
     "olpe_destroy": (None, [_P]),

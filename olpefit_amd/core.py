@@ -266,6 +266,20 @@ class Sampler:
         check(self._lib.olpe_last_units(self._ctx, C.byref(v)))
         return v.value
 
+    # -- devices ----------------------------------------------------------------
+    @staticmethod
+    def device_count() -> int:
+        n = C.c_int(0)
+        check(_lib.load().olpe_device_count(C.byref(n)))
+        return n.value
+
+    @staticmethod
+    def device_pci_id(device: int) -> str:
+        """PCI bus id of a HIP device: tells GPUs apart across processes."""
+        buf = C.create_string_buffer(64)
+        check(_lib.load().olpe_device_pci_id(int(device), buf, 64))
+        return buf.value.decode()
+
     # -- multi-GPU --------------------------------------------------------------
     @staticmethod
     def comm_unique_id() -> bytes:

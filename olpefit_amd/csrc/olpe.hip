@@ -1126,6 +1126,16 @@ int olpe_device_count(int *count) {
   return OLPE_OK;
 }
 
+int olpe_device_pci_id(int device, char *buf, int len) {
+  if (!buf || len < 16) return set_err(OLPE_EINVAL, "buffer of at least 16 bytes needed");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return set_err(OLPE_EHIP, "no HIP device visible");
+  if (device < 0 || device >= ndev) return set_err(OLPE_EINVAL, "bad device %d", device);
+  HIPCHK(hipDeviceGetPCIBusId(buf, len, device));
+  return OLPE_OK;
+}
+
 int olpe_device_mem(int device, long long *free_bytes, long long *total_bytes) {
   if (!free_bytes || !total_bytes) return set_err(OLPE_EINVAL, "NULL argument");
   int ndev = 0;

@@ -34,6 +34,18 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def rank_device(local: int, visible: int) -> int:
+    """HIP device of the rank with LOCAL_RANK ``local`` when the process sees ``visible``
+    devices: its own ordinal when every GPU is visible (torchrun, bench.py --gpus), 0
+    when the launcher gave each process one GPU (HIP_VISIBLE_DEVICES per rank).  Whether
+    the ranks then hold distinct GPUs is checked by PCI bus id (bench.py)."""
+    if visible <= 0 or local < visible:
+        return local
+    if visible == 1:
+        return 0
+    raise ValueError(f"LOCAL_RANK {local} but this process sees {visible} GPUs")
+
+
 def shard(total: int, world: int, rank: int):
     """Contiguous shard [w0, w0 + n) of ``total`` walkers for ``rank`` (strong split;
     shard sizes differ by at most one, so the RCCL gathers, which need equal counts,

@@ -41,6 +41,14 @@ class StubSampler:
     def close(self):
         pass
 
+    @staticmethod
+    def device_count():
+        return int(os.environ.get("OLPE_STUB_NDEV", "8"))
+
+    @staticmethod
+    def device_pci_id(device):
+        return f"0000:{0x10 + device:02x}:00.0"
+
     def chi_squared(self, p):
         return 4096.0
 

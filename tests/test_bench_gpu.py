@@ -64,3 +64,22 @@ def test_bench_gpus_flag_two_ranks_share_gpu():
     assert d["value"] == pytest.approx(2 * 2048 * 100 * 2 / (d["ms_per_step"] * 2e-3),
                                        rel=1e-9)
     assert d["posterior"]["walkers"] == 2 * 2048
+
+
+def test_bench_gpus_two_ranks_need_two_gpus():
+    """Without --share-gpu, two ranks on a one-GPU box would time-share the card (and
+    RCCL refuses them): the ranks compare their devices' PCI bus ids and all exit 4.
+    With two or more GPUs visible the same command runs one rank per GPU."""
+    from olpefit_amd.core import Sampler
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--walkers", "512",
+                        "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-alt"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    if Sampler.device_count() == 1:
+        assert r.returncode == 4, r.stderr[-2000:]
+        assert "ranks share a GPU" in r.stderr
+    else:
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["n_gpus"] == 2 and len(d["config"]["pci_bus_ids"]) == 2

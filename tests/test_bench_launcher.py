@@ -152,3 +152,20 @@ def test_eight_ranks_name_configs3():
     d = _line(r)
     assert d["config"]["workload"].startswith("configs[3]: 524,288 walkers")
     assert d["posterior"]["walkers"] == 524288
+
+
+def test_ranks_on_one_gpu_are_refused_without_share_gpu():
+    # every process sees one GPU: each rank takes device 0 (per-rank visibility), and the
+    # PCI ids show that the ranks share it -> exit 4 on every rank, no line
+    r = _run(["--gpus", "2"], {"OLPE_STUB_NDEV": "1"})
+    assert r.returncode == 4
+    assert "ranks share a GPU" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_rank_device_choice():
+    from olpefit_amd import dist
+    assert [dist.rank_device(r, 8) for r in range(8)] == list(range(8))
+    assert dist.rank_device(3, 1) == 0              # one visible GPU per process
+    with pytest.raises(ValueError):
+        dist.rank_device(5, 4)
