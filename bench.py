@@ -34,6 +34,7 @@ import json
 import multiprocessing as mp
 import os
 import platform
+import signal
 import sys
 import threading
 import time
@@ -285,11 +286,29 @@ def launch_ranks(n: int, argv, grace_s: float = 30.0) -> int:
                 WORLD_SIZE=str(n), OLPE_BENCH_LAUNCHED="1")
     env0.setdefault("TORCHELASTIC_RUN_ID", f"bench-{os.getpid()}-{port}")
     procs = []
+
+    def die_with_parent():
+        # a rank must not outlive the launcher (a killed launcher would leave ranks holding
+        # the GPUs): PR_SET_PDEATHSIG = 1 sends it SIGTERM when the parent dies
+        try:
+            import ctypes
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM, 0, 0, 0)
+        except (OSError, AttributeError):
+            pass
+
+    def stop_all(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, stop_all)
     for r in range(n):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
-                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
-                                      stderr=None, text=True))
+                                      env=env, stdout=subprocess.PIPE if r == 0 else 2,
+                                      stderr=None, text=True, preexec_fn=die_with_parent))
 
     def pump():
         for line in procs[0].stdout:

@@ -169,3 +169,32 @@ def test_rank_device_choice():
     assert dist.rank_device(3, 1) == 0              # one visible GPU per process
     with pytest.raises(ValueError):
         dist.rank_device(5, 4)
+
+
+def test_killed_launcher_takes_its_ranks_along():
+    """SIGTERM to the launcher terminates its ranks (and a rank whose launcher dies gets
+    SIGTERM from the kernel: PR_SET_PDEATHSIG), so no rank outlives it holding a GPU."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OLPE_BENCH_SAMPLER="bench_stub:StubSampler", OLPE_STUB_MS="500",
+               PYTHONPATH=os.pathsep.join([TESTS, REPO]))
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3",
+                          "--walkers", "8", "--steps", "100", "--warmup", "0",
+                          "--no-cpu-baseline", "--no-alt"], cwd=REPO, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    time.sleep(4)
+    kids = subprocess.run(["pgrep", "-P", str(p.pid)], capture_output=True, text=True)
+    pids = [int(x) for x in kids.stdout.split()]
+    assert len(pids) == 3
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=30)
+    assert p.returncode != 0
+    deadline = time.time() + 20
+    while time.time() < deadline and any(os.path.exists(f"/proc/{q}") and
+                                         open(f"/proc/{q}/stat").read().split()[2] != "Z"
+                                         for q in pids):
+        time.sleep(0.2)
+    assert not any(os.path.exists(f"/proc/{q}") and open(f"/proc/{q}/stat").read().split()[2] != "Z"
+                   for q in pids)
