@@ -496,6 +496,13 @@ def test_step3_cli_reads_step2_output(tmp_path, golden, capsys):
         np.testing.assert_allclose(mom["parameters"][k]["gr_rc"], r["gr_rc"], rtol=5e-12)
     with pytest.raises(ValueError):
         step3.main([image, "x", "-s", str(M + 1), "--from-moments", "-q"])
+    # the moments cover every recorded row (additional_burnin 1): a larger -a cannot be
+    # applied to them and is refused instead of being reported as applied
+    with pytest.raises(SystemExit) as ei:
+        step3.main([image, "x", "-s", str(M), "--from-moments", "-a", "3", "-q"])
+    assert ei.value.code == 2
+    assert step3.main([image, "x", "-s", str(M), "--from-moments", "-a", "1", "-q"])[
+        "additional_burnin"] == 1
     # a step-2 run shorter than its burn-in leaves only the NaN seed row: a clear error
     pipeline.write_chain_csvs(paths, np.zeros((M, 0, ps)), nan_row=True)
     with pytest.raises(ValueError, match="none left"):
