@@ -317,6 +317,12 @@ if __name__ == "__main__":
         make_long_case("c64_long", 64, 2, n_walkers=4, accept_min=340, burn_in=0)
         make_long_case("c128_3_long", 128, 3, n_walkers=2, accept_min=90, burn_in=0)
         sys.exit(0)
+    if sys.argv[1:] == ["long2"]:
+        # configs[0]'s shape (32x32, 2 sources) past its 1,000 iterations, and the 3-source
+        # 64x64 cutout past 2,000
+        make_long_case("c32_long", 32, 2, n_walkers=2, accept_min=75, burn_in=0)
+        make_long_case("c64_3_long", 64, 3, n_walkers=2, accept_min=115, burn_in=0)
+        sys.exit(0)
     if sys.argv[1:] == ["nonfinite"]:
         # round 3: cutouts with NaN / -inf / +inf data pixels (the reference's np.ma
         # chi_squared drops them, apf_step2.py:134-137 on the array from :188)

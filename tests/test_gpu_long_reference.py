@@ -2,10 +2,11 @@
 
 tests/golden/make_golden.py ``long`` executed apf_step2.py:298-338 (3body :324-373)
 with astropy 4.3.1 to accept_min 340 (4 walkers, 64x64, 2 sources: ~5,900 iterations
-each) and 90 (2 walkers, 128x128, 3 sources: ~1,900 each), and stored the state after
-every iteration.  The HIP sampler, from the same start and seeds, must give every row
-(FAST and EXACT, the trajectory tolerances of test_gpu_parity.py) and the same accept
-decisions; then the posterior statistics step 3 computes (apf_step3.py:258-278: mean,
+each) and 90 (2 walkers, 128x128, 3 sources: ~1,900 each), and ``long2`` to 75 (2
+walkers, 32x32 -- configs[0]'s shape --: ~1,400 each) and 115 (2 walkers, 64x64, 3
+sources: ~2,550 each), and stored the state after every iteration.  The HIP sampler,
+from the same start and seeds, must give every row (FAST and EXACT, the trajectory
+tolerances of test_gpu_parity.py) and the same accept decisions; then the posterior statistics step 3 computes (apf_step3.py:258-278: mean,
 sigma, Gelman-Rubin RC) over the HIP chains must equal those over the reference's
 chains, and the source centroids must agree within the north star's 1e-3 px (the
 difference is printed).
@@ -36,13 +37,14 @@ def _run(g, mode):
 
 
 @pytest.mark.parametrize("mode", ["fast", "exact"])
-@pytest.mark.parametrize("name", ["c64_long", "c128_3_long"])
+@pytest.mark.parametrize("name", ["c64_long", "c128_3_long", "c32_long", "c64_3_long"])
 def test_long_chains_match_the_reference(golden, name, mode):
     g = golden(name)
     nsrc = int(g["nsrc"])
     chain, tr, L = _run(g, mode)
     ref = g["traj_params"][:, :L]
-    assert L >= (5000 if nsrc == 2 else 1500)
+    assert L >= {"c64_long": 5000, "c128_3_long": 1500, "c32_long": 1000,
+                 "c64_3_long": 2000}[name]
     for w in range(len(g["seeds"])):
         np.testing.assert_array_equal(tr[w, :, 5] != 0, g["traj_acc"][w, :L],
                                       err_msg=f"{name} walker {w}: accept decisions")

@@ -124,7 +124,8 @@ def test_nonfinite_pixels_drop_out(golden, name):
         np.testing.assert_allclose(chi, g["chi2"][k], rtol=1e-12)
 
 
-@pytest.mark.parametrize("name,walker", [("c64_long", 3), ("c128_3_long", 1)])
+@pytest.mark.parametrize("name,walker", [("c64_long", 3), ("c128_3_long", 1),
+                                         ("c32_long", 1), ("c64_3_long", 0)])
 def test_oracle_long_chain_matches_reference(golden, name, walker):
     """The round-4 long fixtures (make_golden.py ``long``: the reference's own loop to
     accept_min 340 / 90): one walker's whole chain (5,775 / 1,945 iterations) from the
