@@ -37,3 +37,15 @@ def golden():
             cache[name] = load_golden(name)
         return cache[name]
     return get
+
+
+@pytest.fixture(scope="session")
+def lib_loaded():
+    """libolpe.so loaded and a GPU visible to it (GPU tests fail, not skip, without)."""
+    import ctypes as C
+    from olpefit_amd import _lib
+    lib = _lib.load()
+    n = C.c_int(0)
+    lib.olpe_device_count(C.byref(n))
+    assert n.value >= 1, "no GPU visible to libolpe"
+    return lib

@@ -36,17 +36,6 @@ def make_sampler(g, mode="exact", **kw):
     return s
 
 
-@pytest.fixture(scope="module")
-def lib_loaded():
-    from olpefit_amd import _lib
-    lib = _lib.load()
-    import ctypes as C
-    n = C.c_int(0)
-    lib.olpe_device_count(C.byref(n))
-    assert n.value >= 1, "no GPU visible to libolpe"
-    return lib
-
-
 def test_rng_streams_bit_exact(golden, lib_loaded):
     g = golden("rng")
     img = golden("c32")
