@@ -198,3 +198,29 @@ def test_killed_launcher_takes_its_ranks_along():
         time.sleep(0.2)
     assert not any(os.path.exists(f"/proc/{q}") and open(f"/proc/{q}/stat").read().split()[2] != "Z"
                    for q in pids)
+
+
+def test_driver_launch_form_under_torchrun():
+    """The driver's scaling command, `python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`:
+    the ranks come from torchrun's environment (the bench starts none itself) and rank 0
+    prints the whole job's line."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT",
+                        "TORCHELASTIC_RUN_ID", "OLPE_BENCH_LAUNCHED")}
+    env.update(OLPE_BENCH_SAMPLER="bench_stub:StubSampler", OLPE_STUB_MS="5",
+               PYTHONPATH=os.pathsep.join([TESTS, REPO]))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--walkers", str(WPG), "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-alt"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r)
+    assert d["n_gpus"] == 2 and d["config"]["launcher"] == "environment"
+    assert d["config"]["local_ranks"] == [0, 1] and d["allgather_ms"] is not None
