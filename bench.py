@@ -282,19 +282,23 @@ def launch_ranks(n: int, argv, grace_s: float = 30.0) -> int:
     import subprocess
     env0 = dict(os.environ)
     port = _free_port()
-    env0.update(MASTER_ADDR=env0.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port),
-                WORLD_SIZE=str(n), OLPE_BENCH_LAUNCHED="1")
+    # one node: the ranks meet on the loopback address whatever MASTER_ADDR says
+    env0.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                OLPE_BENCH_LAUNCHED="1")
     env0.setdefault("TORCHELASTIC_RUN_ID", f"bench-{os.getpid()}-{port}")
     procs = []
 
+    try:
+        import ctypes
+        prctl = ctypes.CDLL(None, use_errno=True).prctl
+    except (OSError, AttributeError):
+        prctl = None
+
     def die_with_parent():
-        # a rank must not outlive the launcher (a killed launcher would leave ranks holding
-        # the GPUs): PR_SET_PDEATHSIG = 1 sends it SIGTERM when the parent dies
-        try:
-            import ctypes
-            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM, 0, 0, 0)
-        except (OSError, AttributeError):
-            pass
+        # (in the child between fork and exec) a rank must not outlive the launcher, or
+        # a killed launcher would leave ranks holding the GPUs: PR_SET_PDEATHSIG (1)
+        if prctl is not None:
+            prctl(1, signal.SIGTERM, 0, 0, 0)
 
     def stop_all(signum, _frame):
         for p in procs:
