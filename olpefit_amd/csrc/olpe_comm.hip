@@ -130,7 +130,10 @@ int olpe_comm_allgather_state(olpe_ctx *c, double *out) {
   const size_t per = (size_t)c->W * c->ps;
   double *d = nullptr;
   // allocate first; the outcome travels in the uniformity check
-  if (hipMalloc(&d, per * c->nranks * sizeof(double)) != hipSuccess) d = nullptr;
+  if (hipMalloc(&d, per * c->nranks * sizeof(double)) != hipSuccess) {
+    d = nullptr;
+    (void)hipGetLastError();     // so that a later launch check does not report it
+  }
   int rc;
   if ((rc = check_uniform(c, 0, true, 0, 0, false, d == nullptr))) {
     if (d) (void)hipFree(d);
@@ -172,6 +175,7 @@ int olpe_comm_allgather_chain(olpe_ctx *c, long long w0, long long wn, double *o
     if ((ae = hipMalloc(&c->d_gather, need * sizeof(double))) != hipSuccess) {
       c->d_gather = nullptr;
       alloc_failed = true;
+      (void)hipGetLastError();
     } else {
       c->gather_cap = need;
     }
@@ -210,7 +214,10 @@ int olpe_comm_allreduce_moments(olpe_ctx *c, double *out) {
   const int ps = c->ps;
   const size_t len = (size_t)OLPE_MOMENTS_LEN(ps, c->np);
   double *d = nullptr;
-  if (hipMalloc(&d, (len + ps) * sizeof(double)) != hipSuccess) d = nullptr;
+  if (hipMalloc(&d, (len + ps) * sizeof(double)) != hipSuccess) {
+    d = nullptr;
+    (void)hipGetLastError();
+  }
   // a sum needs equal row counts (step 3's N), not equal shards
   int rc = c->comm ? check_uniform(c, c->mom_n, false, 0, 0, false, d == nullptr)
                    : d ? OLPE_OK : set_err(OLPE_ENOMEM, "hipMalloc for the moments summary");
