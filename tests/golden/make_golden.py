@@ -160,7 +160,10 @@ def bad_pixels(n, nsrc):
     g = synth.guess_values(n, nsrc)
     rs, cs = int(g[1] - 1), int(g[0] - 1)
     rc, cc = int(g[3] - 1), int(g[2] - 1)
-    return [(rs - 2, cs - 1, np.nan), (rs - 2, cs + 2, -np.inf), (rc + 1, cc + 1, np.nan),
+    # (the 3-source script reads its amplitudes at int(y + 0.5), int(x + 0.5), i.e. one
+    # pixel further, 3body/apf_step2_3body.py:258-260: keep that pixel finite too)
+    dc = 2 if nsrc == 3 else 1
+    return [(rs - 2, cs - 1, np.nan), (rs - 2, cs + 2, -np.inf), (rc + dc, cc + 1, np.nan),
             (rc - 1, cc, -np.inf), (n - 3, n - 5, -np.inf), (n // 2 + 6, 4, np.nan),
             (n - 2, 3, np.inf)]
 
@@ -322,6 +325,13 @@ if __name__ == "__main__":
         # 64x64 cutout past 2,000
         make_long_case("c32_long", 32, 2, n_walkers=2, accept_min=75, burn_in=0)
         make_long_case("c64_3_long", 64, 3, n_walkers=2, accept_min=115, burn_in=0)
+        sys.exit(0)
+    if sys.argv[1:] == ["nonfinite3"]:
+        # round 4: the 3-source twins with non-finite data pixels (3body
+        # apf_step2_3body.py's chi_squared is the same np.ma arithmetic)
+        make_case("c64_3_nan", 64, 3, n_walkers=2, accept_min=20, burn_in=0, nonfinite=True)
+        make_case("c128_3_nan", 128, 3, n_walkers=2, accept_min=6, burn_in=0, n_model=4,
+                  nonfinite=True)
         sys.exit(0)
     if sys.argv[1:] == ["nonfinite"]:
         # round 3: cutouts with NaN / -inf / +inf data pixels (the reference's np.ma

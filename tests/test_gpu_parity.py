@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 # *_nan: NaN / -inf / +inf data pixels, dropped by the reference's np.ma chi_squared
 # (apf_step2.py:134-137; fixtures from make_golden.py ``nonfinite``)
-CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan"]
+CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan", "c64_3_nan", "c128_3_nan"]
 
 
 def make_sampler(g, mode="exact", **kw):
@@ -135,14 +135,14 @@ def test_trajectories_match_reference(golden, lib_loaded, name, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("name", ["c32_nan", "c64_nan"])
+@pytest.mark.parametrize("name", ["c32_nan", "c64_nan", "c64_3_nan", "c128_3_nan"])
 def test_nonfinite_pixels_dropped_by_the_library(golden, lib_loaded, name, mode):
     """olpe_create drops NaN / -inf data pixels by itself: given only the reference's
     saturation mask (np.ma.masked_greater, apf_step2.py:188), which does not cover them,
     chi^2 still equals the reference's finite values."""
     from olpefit_amd.core import Sampler
     g = golden(name)
-    s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=2, mask=g["mask"])
+    s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=int(g["nsrc"]), mask=g["mask"])
     s.set_eval_mode(mode)
     chi = s.chi_squared(g["params"])
     assert np.all(np.isfinite(chi))

@@ -15,7 +15,7 @@ from oracle.legacy_rng import LegacyMT
 
 # *_nan: the c32 / c64 cutouts with NaN, -inf and +inf data pixels (make_golden.py
 # ``nonfinite``): the reference's np.ma chi_squared drops them (apf_step2.py:134-137)
-CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan"]
+CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan", "c64_3_nan", "c128_3_nan"]
 
 
 def test_rng_numpy_stream_frozen(golden):
