@@ -22,9 +22,11 @@ def test_metric_is_baselines():
         assert bench.METRIC == json.load(f)["metric"]
 
 
-@pytest.mark.parametrize("name,cfg", [("bench", 2), ("bench_c1", 1), ("bench_c4", 4)])
-def test_committed_bench_lines(name, cfg):
-    d = _last_json(os.path.join(REPO, "profiles", "r03", f"{name}.log"))
+@pytest.mark.parametrize("where,name,cfg", [
+    ("r03", "bench", 2), ("r03", "bench_c1", 1), ("r03", "bench_c4", 4),
+    ("r04/final", "bench", 2), ("r04/final", "bench_c1", 1), ("r04/final", "bench_c4", 4)])
+def test_committed_bench_lines(where, name, cfg):
+    d = _last_json(os.path.join(REPO, "profiles", where, f"{name}.log"))
     assert d["metric"] == bench.METRIC and d["unit"] == "walker-steps/s"
     assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["dtype"] == "f64" and d["vs_baseline"] is None
@@ -53,3 +55,23 @@ def test_committed_bench_lines(name, cfg):
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "walker-steps/s" and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["sample"]
+    if where.startswith("r04"):
+        # round 4: SURVEY 8(d)'s shape per config, the reference/port ratio, the held clock
+        dflt = bench.DEFAULTS[cfg]
+        assert c["iters_per_step"] == dflt["iters"] and c["chain_stride"] == dflt["stride"]
+        assert d["steps"] * c["iters_per_step"] == {1: 10000, 2: 2000, 4: 500}[cfg]
+        assert p["tag"] == "r04" and 0 < p["frac_of_held_clock_peak"] < 1
+        assert 0 < cb["reference_over_port"] < 1
+        assert d["gpu_over_reference"] == pytest.approx(
+            d["value"] / (cb["value"] * cb["reference_over_port"]), rel=1e-9)
+        assert c["devices"] == [0] and c["launcher"] == "none (1 rank)"
+
+
+def test_committed_config0_line():
+    """configs[0] (1 walker, 32x32, 1,000 iterations): the GPU's one walker beside the
+    oracle's one walker on one core (profiles/r04/final/bench_c0.log)."""
+    d = _last_json(os.path.join(REPO, "profiles", "r04", "final", "bench_c0.log"))
+    c = d["config"]
+    assert c["walkers_per_gpu"] == 1 and c["image"] == "32x32" and c["iters_per_step"] == 1000
+    assert d["steps"] == 1 and d["cpu_baseline"]["cores"] == 1
+    assert d["value"] > d["cpu_baseline"]["value"] > d["cpu_baseline"]["reference_value_derived"]
