@@ -10,7 +10,7 @@ from olpefit_amd import fitsio, pipeline, step3, synth
 from oracle import olpe_oracle as ora
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["c32", "c64", "c64_3", "c128_3"]
+CASES = ["c32", "c64", "c64_3", "c128_3", "c32_nan", "c64_nan", "c64_3_nan", "c128_3_nan"]
 
 
 def _rows_and_counters(g, w):
@@ -297,6 +297,12 @@ def test_native_acceptance_files_equal_numpy_str(tmp_path):
     for w in range(W):
         pipeline.write_acceptance(b[w], acc[w], tries[w])
         assert open(a[w], "rb").read() == open(b[w], "rb").read(), w
+    # written to a temporary name and renamed over the file (a kill mid-write
+    # leaves the previous file): rewriting replaces every file whole, no .tmp is left
+    old = {w: open(a[w], "rb").read() for w in range(W)}
+    pipeline.write_acceptance_files(a, acc + 1, tries + 2, threads=4)
+    assert not list(tmp_path.glob("*.tmp"))
+    assert all(open(a[w], "rb").read() != old[w] for w in range(W) if w != 3)
 
 
 def test_native_csv_formatter_equals_repr():
