@@ -53,12 +53,28 @@ CONFIGS = {
     2: (65536, 64, 2),
     4: (16384, 128, 3),
 }
+CONFIGS[3] = CONFIGS[2]               # configs[3] = configs[2]'s 65,536 walkers on each of 8 GPUs
 CONFIG_NAMES = {
     0: "configs[0]: 1 walker, 32x32 2-source cutout, 1,000 iterations (plumbing reference)",
     1: "configs[1]: 4,096 walkers, 64x64 2-source cutout, fp64",
     2: "configs[2]: 65,536 walkers/GPU, 64x64 2-source cutout, fp64, LDS-resident image",
     4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
 }
+CONFIG3 = ("configs[3]: 524,288 walkers sharded 8 x MI355X (65,536 per GPU, 64x64 2-source "
+           "cutout, fp64), RCCL chain all-gather at the end")
+
+
+def workload_name(config: int, world: int, wpg: int) -> str:
+    """The line's ``config.workload``: configs[2] at 8 ranks of 65,536 walkers is
+    configs[3] (``--config 3`` names it too, and on fewer GPUs says which part ran)."""
+    if config in (2, 3) and world == 8 and wpg == 65536:
+        return CONFIG3
+    if config == 3:
+        return (f"configs[3]'s per-GPU shards on {world} GPU{'s' if world > 1 else ''} "
+                f"({world} x {wpg:,} of 524,288 walkers; the whole of configs[3] is --gpus 8)")
+    return CONFIG_NAMES[config]
+
+
 # SURVEY.md 8(d)'s run of each config: iterations per launch (a bench step), chain record
 # stride ("every step for configs 1-2 and with stride 10 otherwise"), timed steps and
 # warm-up steps, so that the timed steps cover the config's iteration count: configs[0]
@@ -69,6 +85,7 @@ DEFAULTS = {
     2: dict(iters=100, stride=10, steps=20, warmup=5),
     4: dict(iters=100, stride=10, steps=5, warmup=2),
 }
+DEFAULTS[3] = DEFAULTS[2]
 # BASELINE.json's metric, character for character (its "64\u00d764")
 METRIC = "walker-steps/sec (= model evals/sec) on 64\u00d764 2-source cutout, 1/2/4/8 GPU"
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
@@ -506,7 +523,7 @@ def main():
         digest = kernel_digest()
 
         def key(mode):
-            return mode if args.config == 2 else f"c{args.config}_{mode}"
+            return mode if args.config in (2, 3) else f"c{args.config}_{mode}"
 
         def roofline(mode, kernel_ms):
             """FP64-VALU roofline of the sampler kernel.  frac: executed
@@ -587,10 +604,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
-            "config": {"workload": (CONFIG_NAMES[args.config] if not (
-                           args.config == 2 and world == 8 and wpg == 65536) else
-                           "configs[3]: 524,288 walkers sharded 8 x MI355X (65,536 per GPU, "
-                           "64x64 2-source cutout, fp64), RCCL chain all-gather at the end"),
+            "config": {"workload": workload_name(args.config, world, wpg),
                        "walkers_per_gpu": wpg,
                        "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                        "chain_stride": args.stride, "eval": args.mode,

@@ -130,7 +130,7 @@ def test_per_config_defaults_cover_the_survey_runs():
     # configs[0] 1,000 iterations, [1] 10,000 at stride 1, [2] 2,000 at
     # stride 10, [4] 500 at stride 10
     tot = {k: v["iters"] * v["steps"] for k, v in bench.DEFAULTS.items()}
-    assert tot == {0: 1000, 1: 10000, 2: 2000, 4: 500}
+    assert tot == {0: 1000, 1: 10000, 2: 2000, 3: 2000, 4: 500}
     assert [bench.DEFAULTS[k]["stride"] for k in (0, 1, 2, 4)] == [1, 1, 10, 10]
 
 
@@ -224,3 +224,11 @@ def test_driver_launch_form_under_torchrun():
     d = _line(r)
     assert d["n_gpus"] == 2 and d["config"]["launcher"] == "environment"
     assert d["config"]["local_ranks"] == [0, 1] and d["allgather_ms"] is not None
+
+
+def test_config3_names_its_part():
+    r = _run(["--config", "3", "--gpus", "2", "--walkers", "65536", "--steps", "1"],
+             {"OLPE_STUB_MS": "1"})
+    assert r.returncode == 0, r.stderr
+    w = _line(r)["config"]["workload"]
+    assert w.startswith("configs[3]'s per-GPU shards on 2 GPUs") and "--gpus 8" in w
