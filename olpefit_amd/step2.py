@@ -460,7 +460,20 @@ def main(argv=None, nsrc=2, variant="2"):
     if pW < 1:
         raise ValueError(f"{W} walkers over {world} ranks: rank {rank} has none")
     ng = max(1, min(args.gpus, pW))
-    dev0 = args.device + (0 if args.share_gpu else local * ng)
+    if args.share_gpu:
+        dev0 = args.device
+    elif ng == 1 and world > 1:
+        # one GPU per rank: LOCAL_RANK's device, or device 0 when the launcher gave each
+        # process its own GPU (as bench.py; dist.rank_device), and no two ranks on one
+        # GPU unless --share-gpu says so (PCI bus ids, the same verdict on every rank)
+        from .core import Sampler
+        dev0 = args.device + dist.rank_device(local, Sampler.device_count() - args.device)
+        pci = group.allgather(Sampler.device_pci_id(dev0))
+        if len(set(pci)) < world:
+            raise RuntimeError(f"ranks share a GPU (PCI {pci}): one process per GPU needs as "
+                               "many GPUs as ranks (--share-gpu for a rehearsal on fewer)")
+    else:
+        dev0 = args.device + local * ng
     bounds = [pw0 + (g * pW) // ng for g in range(ng + 1)]
     shards = [Shard(image, hdr, nsrc, dev0 + g, bounds[g], bounds[g + 1] - bounds[g], p0,
                     seeds, args.exact, 1 if args.fixed_bkgd else 0) for g in range(ng)]
