@@ -1,6 +1,6 @@
 """Benchmark: walker-steps/s of the apf_step2 Gibbs/MH hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--mode exact|fast]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 0-4] [--mode exact|fast]
 
 A bench *step* is one launch of the fused sampler kernel: every walker on the GPU
 runs ``--iters`` Gibbs iterations (apf_step2.py:300-351: parameter draw, proposal,
@@ -9,14 +9,17 @@ iterations into an HBM chain buffer.  Inputs (cutout, sigma map, walker state, R
 state) are resident in HBM before the timed region.
 
 Workload (BASELINE.json configs[2]): 65,536 walkers per
-GPU on a synthetic 64x64 two-source NIRC2 cutout, fp64, chain stride 10.  For N > 1
-GPUs the driver launches one process per GPU (torch.distributed.run); walkers are
-sharded with seeds 1000 + global walker index, there is no communication while
-sampling, and the end-of-run RCCL exchange (outside the timed region) is the only
-one: all-gather of the final states (``allgather_ms``) and the chain concatenation
-(all-gather of the last launch's chain rows over xGMI, in walker ranges that bound the
-receive buffer: ``chain_gather_ms`` / ``_bytes`` / ``_gbs``).  ``scaling`` is "weak".
-The host group (barrier, max-over-ranks time, RCCL id) is stdlib TCP, no PyTorch.
+GPU on a synthetic 64x64 two-source NIRC2 cutout, fp64, 20 launches of 100 iterations
+at chain stride 10 (``--config 0 / 1 / 3 / 4``: the other configs at their §8(d) runs,
+``DEFAULTS``).  N > 1 GPUs run one process per GPU: ``--gpus N`` starts the N ranks
+itself when no launcher did (``launch_ranks``), or takes them from torchrun / mpirun
+(``WORLD_SIZE`` must equal N).  Walkers are sharded with seeds 1000 + global walker
+index, there is no communication while sampling, and the end-of-run RCCL exchange
+(outside the timed region) is the only one: all-gather of the final states
+(``allgather_ms``) and the chain concatenation (all-gather of the last launch's chain
+rows over xGMI, in walker ranges that bound the receive buffer: ``chain_gather_ms`` /
+``_bytes`` / ``_gbs``).  ``scaling`` is "weak".  The host group (barrier,
+max-over-ranks time, RCCL id) is stdlib TCP, no PyTorch.
 
 Roofline: the kernel is FP64-VALU bound.  ``roofline.frac`` = executed
 FP64 VALU lane-ops per second / 39.3e12 (78.6 TFLOP/s with FMA = 2), the executed
