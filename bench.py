@@ -243,12 +243,34 @@ def reference_ratio(n: int, nsrc: int, path: str):
             "timing_file": os.path.relpath(path, REPO)}
 
 
+# stdout carries exactly one line, the JSON: RCCL prints its banner ("RCCL version ...")
+# to stdout when a communicator is created, so the exchange runs with fd 1 pointed at
+# stderr (``_quiet_stdout``) and fd 1 is restored before anything is printed
+_SAVED_STDOUT = None
+
+
+def _quiet_stdout():
+    global _SAVED_STDOUT
+    sys.stdout.flush()
+    _SAVED_STDOUT = os.dup(1)
+    os.dup2(2, 1)
+
+
+def _restore_stdout():
+    global _SAVED_STDOUT
+    fd, _SAVED_STDOUT = _SAVED_STDOUT, None
+    if fd is not None:
+        os.dup2(fd, 1)
+        os.close(fd)
+
+
 def _comm_timeout(rank: int, make_report, timeout: float):
     """Watchdog of the end-of-run RCCL exchange: rank 0 prints the measurement with the
     error, then every rank leaves with status 3 (os._exit: the hung collective never
     returns; the launcher and CI see the failure, the JSON line keeps the numbers)."""
     print(f"[bench rank {rank}] RCCL exchange still running after {timeout:g} s: giving up",
           file=sys.stderr)
+    _restore_stdout()
     if rank == 0:
         out = make_report()
         out["comm_error"] = f"TimeoutError: RCCL exchange did not finish within {timeout:g} s"
@@ -654,6 +676,7 @@ def main():
                                                          dict(comm)), args.comm_timeout))
         watchdog.daemon = True
         watchdog.start()
+        _quiet_stdout()
         try:
             uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
             s.comm_init(uid, world, rank)
@@ -697,6 +720,8 @@ def main():
             comm["comm_error"] = f"{type(e).__name__}: {e}"
             print(f"[bench rank {rank}] RCCL exchange failed: {comm['comm_error']}",
                   file=sys.stderr)
+        finally:
+            _restore_stdout()
 
     if world > 1 and args.share_gpu and not args.no_moments:
         # ranks sharing one GPU have no RCCL: their moments are summed over the host

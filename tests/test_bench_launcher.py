@@ -60,6 +60,9 @@ def test_gpus_flag_spawns_n_ranks(n):
     assert d["posterior"]["walkers"] == n * WPG
     assert d["posterior"]["rows_per_walker"] == (STEPS + 1) * nrec
     assert "cpu_baseline" not in d                     # rank 0 at N = 1 only
+    # stdout is the JSON line alone: the communicator's banner went to stderr
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == [r.stdout.strip()]
+    assert "RCCL version : stub banner" in r.stderr
 
 
 def test_chain_gather_ranges_and_verify():
