@@ -252,14 +252,26 @@ _SAVED_STDOUT = None
 def _quiet_stdout():
     global _SAVED_STDOUT
     sys.stdout.flush()
+    _libc_fflush()
     _SAVED_STDOUT = os.dup(1)
     os.dup2(2, 1)
+
+
+def _libc_fflush():
+    # C stdio buffers what the library printed (RCCL's banner goes through printf): flush
+    # it while fd 1 still points at stderr
+    try:
+        import ctypes
+        ctypes.CDLL(None).fflush(None)
+    except (OSError, AttributeError):
+        pass
 
 
 def _restore_stdout():
     global _SAVED_STDOUT
     fd, _SAVED_STDOUT = _SAVED_STDOUT, None
     if fd is not None:
+        _libc_fflush()
         os.dup2(fd, 1)
         os.close(fd)
 

@@ -98,7 +98,10 @@ class StubSampler:
     def comm_init(self, uid, nranks, rank):
         # RCCL prints a banner to stdout when a communicator is created (fd 1, not
         # sys.stdout): the bench must keep it off its one-line stdout
-        os.write(1, b"RCCL version : stub banner\n")
+        # (through C stdio, buffered, as RCCL's printf is)
+        import ctypes
+        libc = ctypes.CDLL(None)
+        libc.printf(b"RCCL version : stub banner\n")
         if uid != b"s" * 128:
             raise StubError("unique id not broadcast")
         self.nranks, self.rank = nranks, rank
