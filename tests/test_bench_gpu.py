@@ -17,6 +17,8 @@ def _bench(*args, timeout=300):
     r = subprocess.run([sys.executable, "bench.py", *args], cwd=REPO, capture_output=True,
                        text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
+    # stdout is the one JSON line (RCCL's banner goes to stderr during the exchange)
+    assert len([ln for ln in r.stdout.splitlines() if ln.strip()]) == 1, r.stdout[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
