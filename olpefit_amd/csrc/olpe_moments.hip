@@ -43,18 +43,30 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWalkersPerBlock = 256;    // summary stage 1: walkers per block
 
-// fold the launch's rows chain[W][nrec][ps] into the running (mean, M2) [ps][W];
-// thread t = w * ps + k reads column k of walker w's rows (consecutive threads read
-// consecutive doubles of a row, consecutive rows follow each other in memory).  One
-// pass over HBM: the rows are taken in blocks of kFoldRows held in registers, each
-// block's (mean, M2) formed by two passes over the registers (mean about its first
-// value, then the squared deviations about that mean) and merged into the thread's
-// running pair with Chan's update -- the two-pass arithmetic without a second read of
-// the launch's rows (at stride 1 the first form's second pass cost configs[1] 3.5 %)
+// fold the launch's rows chain[W][nrec][ps] into the running (mean, M2) [ps][W].
+// One wave per walker: lane l = g * ps + k (g < G = 64 / ps row groups, 3 for 17 or 20
+// columns) reads column k of rows g, g + G, g + 2G, ..., so each load instruction of the
+// wave reads G consecutive rows -- G * ps * 8 contiguous bytes -- and a lane keeps
+// kWaveRows loads in flight (one pass over HBM, each walker's rows streamed in order).
+// (Round 3's kernel ran one thread per (walker, column): a wave's loads then touched
+// four walkers 136 KB apart at stride 1, 3.4 TB/s on configs[1]'s 557 MB of rows.)  A
+// lane's rows are taken in blocks of kWaveRows held in registers, each block's (mean,
+// M2) formed by two passes over the registers (mean about its first value, then the
+// squared deviations about that mean) and merged into the lane's running pair with
+// Chan's update; the G row groups are then merged across lanes the same way, and the
+// walker's pair merged into the running moments -- the two-pass arithmetic without a
+// second read of the rows.
 constexpr int kFoldRows = 8;
+constexpr int kFoldWaves = 4;            // walkers (waves) per fold block
+constexpr int kWaveRows = 16;            // loads in flight per lane (rows per block)
+// launches of fewer rows per walker fold one thread per (walker, column) instead
+// (fold_cols_kernel): a wave per walker has too little to read there (configs[2]'s 10
+// rows: 48 us against 30 us per launch)
+constexpr long long kFoldRowsMin = 64;
 
 __device__ __forceinline__ void chan_merge(double &m, double &q, double &n, double mb,
                                            double qb, double nb) {
+  if (nb == 0.0) return;
   if (n == 0.0) {
     m = mb;
     q = qb;
@@ -68,7 +80,65 @@ __device__ __forceinline__ void chan_merge(double &m, double &q, double &n, doub
   n = nn;
 }
 
-__global__ __launch_bounds__(kThreads) void fold_kernel(const double *__restrict__ chain,
+__global__ __launch_bounds__(64 * kFoldWaves) void fold_rows_kernel(
+    const double *__restrict__ chain, long long W, int ps, long long nrec, double n_a,
+    double *__restrict__ mean, double *__restrict__ m2) {
+  const int lane = threadIdx.x & 63;
+  const long long w = (long long)blockIdx.x * kFoldWaves + (threadIdx.x >> 6);
+  if (w >= W) return;                      // (whole waves: w is wave-uniform)
+  const int G = 64 / ps;
+  const int g = lane / ps;
+  const int k = lane - g * ps;
+  const bool act = g < G;
+  const double *x = chain + (size_t)w * nrec * ps + (act ? g * ps + k : 0);
+  const long long step = (long long)G * ps;           // doubles per row-group step
+  double m = 0.0, q = 0.0, n = 0.0;
+  for (long long r0 = 0; r0 < nrec; r0 += (long long)G * kWaveRows) {
+    double v[kWaveRows];
+    int nb = 0;
+#pragma unroll
+    for (int i = 0; i < kWaveRows; ++i) {
+      const bool ok = act && r0 + g + (long long)i * G < nrec;
+      v[i] = ok ? x[(size_t)(r0 / G) * step + (size_t)i * step] : 0.0;
+      nb += ok ? 1 : 0;
+    }
+    if (nb == 0) continue;
+    const double c = v[0];
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < kWaveRows; ++i) s += i < nb ? v[i] - c : 0.0;
+    const double fb = (double)nb;
+    const double mb = c + s / fb;
+    double qb = 0.0;
+#pragma unroll
+    for (int i = 0; i < kWaveRows; ++i) {
+      const double d = v[i] - mb;
+      qb = i < nb ? fma(d, d, qb) : qb;
+    }
+    chan_merge(m, q, n, mb, qb, fb);
+  }
+  // the row groups of each column into group 0 (lane k), in group order
+  for (int h = 1; h < G; ++h) {
+    const int src = k + h * ps;
+    const double mh = __shfl(m, src), qh = __shfl(q, src), nh = __shfl(n, src);
+    if (g == 0) chan_merge(m, q, n, mh, qh, nh);
+  }
+  if (g != 0) return;
+  const size_t o = (size_t)k * W + w;
+  if (n_a == 0.0) {
+    mean[o] = m;
+    m2[o] = q;
+    return;
+  }
+  double ma = mean[o], qa = m2[o], na = n_a;
+  chan_merge(ma, qa, na, m, q, n);
+  mean[o] = ma;
+  m2[o] = qa;
+}
+
+// one thread t = w * ps + k per (walker, column), rows in blocks of kFoldRows (round 3's
+// fold; kept for short launches)
+__global__ __launch_bounds__(kThreads) void fold_cols_kernel(const double *__restrict__ chain,
                                                         long long W, int ps, long long nrec,
                                                         double n_a, double *__restrict__ mean,
                                                         double *__restrict__ m2) {
@@ -241,10 +311,16 @@ int olpe_moments_accumulate(olpe_ctx *c) {
   c->mom_folded = c->launches;
   const long long nrec = c->chain_rows;
   if (nrec == 0) return OLPE_OK;
-  const long long total = (long long)c->W * c->ps;
-  hipLaunchKernelGGL(fold_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, c->stream, c->d_chain, (long long)c->W, c->ps, nrec,
-                     (double)c->mom_n, c->d_mmean, c->d_mm2);
+  if (nrec >= kFoldRowsMin && c->ps <= 64) {
+    hipLaunchKernelGGL(fold_rows_kernel, dim3((unsigned)((c->W + kFoldWaves - 1) / kFoldWaves)),
+                       dim3(64 * kFoldWaves), 0, c->stream, c->d_chain, (long long)c->W, c->ps,
+                       nrec, (double)c->mom_n, c->d_mmean, c->d_mm2);
+  } else {
+    const long long total = (long long)c->W * c->ps;
+    hipLaunchKernelGGL(fold_cols_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, c->stream, c->d_chain, (long long)c->W, c->ps, nrec,
+                       (double)c->mom_n, c->d_mmean, c->d_mm2);
+  }
   HIPCHK(hipGetLastError());
   c->mom_n += nrec;
   return OLPE_OK;
