@@ -1253,3 +1253,29 @@ def test_moments_fold_matches_numpy(golden, lib_loaded):
         x.moments_accumulate()
     for a, b in zip(s.moments(), t.moments()):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["c32", "c64_3"])
+def test_moments_fold_long_launches(golden, lib_loaded, name):
+    """The one-wave-per-walker fold (launches of >= 64 rows per walker, round 4) beside
+    the column fold (shorter ones), in one accumulation: launches of 97, 5, 64, 150 and
+    63 rows (row counts that leave the wave's 3 row groups and 16-row blocks ragged), 2-
+    and 3-source column counts (17, 20), 37 walkers (a last block of one wave).  Every
+    walker's running mean and M2 equal NumPy's over the concatenated rows."""
+    g = golden(name)
+    W = 37
+    s = make_sampler(g, "fast")
+    s.seed(np.arange(500, 500 + W))
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    parts = []
+    for n in (97, 5, 64, 150, 63):
+        parts.append(s.run(n, burn_in=0, record_stride=1))
+        s.moments_accumulate()
+    chain = np.concatenate(parts, axis=1)
+    nrow, mean, m2 = s.moments()
+    assert nrow == chain.shape[1] == 379
+    ref_mean = chain.mean(axis=1)
+    ref_m2 = ((chain - ref_mean[:, None, :]) ** 2).sum(axis=1)
+    np.testing.assert_allclose(mean, ref_mean, rtol=1e-13)
+    slack = nrow * (10 * np.finfo(float).eps * np.abs(ref_mean)) ** 2
+    assert np.all(np.abs(m2 - ref_m2) <= 1e-10 * np.abs(ref_m2) + slack)
