@@ -227,6 +227,55 @@ def cpu_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None):
                       f"cpu: {model}"}
 
 
+CONDA_PY = "/opt/conda/bin/python3.9"       # the image's python with astropy 4.3.1
+
+
+def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None):
+    """The reference's own loop cost on this box's cores: ``procs`` processes of
+    oracle/astropy_timing.py (the oracle's walker with every Gaussian built as an
+    astropy ``Gaussian2D`` object per proposal, as apf_step2.py:98-102 does; its chains
+    are bit-equal to the reference's own, tests/test_oracle_golden.py), started
+    together after their imports, ``total_iters`` walker-steps in all.  None when the
+    image's python3.9 / astropy is missing."""
+    import subprocess
+    if not os.path.exists(CONDA_PY):
+        return None
+    cores, aff, quota, model = host_cpus()
+    procs = procs or cores
+    iters = max(100, total_iters // procs)
+    script = os.path.join(REPO, "oracle", "astropy_timing.py")
+    ps = [subprocess.Popen([CONDA_PY, script, str(n), str(nsrc), str(1000 + i), str(iters),
+                            "--sync"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                           stderr=subprocess.DEVNULL, text=True) for i in range(procs)]
+    res = []
+    try:
+        # every process imported astropy and warmed up: start their loops together
+        if any(p.stdout.readline().strip() != "ready" for p in ps):
+            return None
+        for p in ps:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        for p in ps:
+            out, _ = p.communicate(timeout=600)
+            if p.returncode != 0:
+                return None
+            res.append(json.loads(out.strip().splitlines()[-1]))
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    secs = max(r["seconds"] for r in res)
+    return {"value": procs * iters / secs, "unit": "walker-steps/s", "cores": procs,
+            "kind": "port (astropy Gaussian2D objects per proposal, as the reference)",
+            "sample": f"oracle/astropy_timing.py under {CONDA_PY} (astropy 4.3.1): {procs} "
+                      f"processes started together x 1 walker x {iters} iterations, {n}x{n} "
+                      f"{nsrc}-source cutout ({sum(r['seconds'] for r in res):.1f} s CPU); "
+                      f"cpu: {model}",
+            "pinned": "chains bit-equal to the reference's own loop "
+                      "(tests/test_oracle_golden.py::test_astropy_oracle_is_the_reference)"}
+
+
 def reference_ratio(n: int, nsrc: int, path: str):
     """The reference's own apf_step2 loop against the port on one core of the build
     container (tests/golden/time_reference.py --json; the reference cannot travel to the
@@ -431,6 +480,11 @@ def main():
                          "core (default: about 12 s of CPU work: 96,000 at 64x64, scaled by "
                          "64^2/n^2 otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reference-like", action="store_true",
+                    help="skip the astropy-object (reference-cost) CPU baseline")
+    ap.add_argument("--cpu-steps-ref", type=int, default=None,
+                    help="walker-steps of the astropy-object baseline in all (default 24,000 "
+                         "at 64x64, scaled by 64^2/n^2)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--reference-timing",
                     default=os.path.join(REPO, "profiles", "r04", "reference_cpu_timing.json"))
@@ -778,6 +832,15 @@ def main():
               else cpu_baseline(n, nsrc, cpu_steps))
         out["cpu_baseline"] = cb
         out["gpu_over_cpu"] = value / cb["value"]
+        if not args.no_reference_like:
+            rl = (reference_like_baseline(n, nsrc, 1000, procs=1) if args.config == 0
+                  else reference_like_baseline(n, nsrc, args.cpu_steps_ref or max(
+                      1600, 24000 * 64 * 64 // (n * n))))
+            if rl:
+                # the reference's loop cost measured on these cores (the astropy-object
+                # oracle), beside the NumPy port above
+                cb["reference_like"] = rl
+                out["gpu_over_reference_like"] = value / rl["value"]
         ref = reference_ratio(n, nsrc, args.reference_timing)
         if ref:
             # the reference itself is slower than the port on the same core: its rate on

@@ -81,6 +81,27 @@ def gaussian2d(x, y, amplitude, x_mean, y_mean, x_stddev, y_stddev, theta):
                                 (c * ydiff ** 2)))
 
 
+#: the Gaussian evaluator build_2d_gaussian calls (use_astropy_models swaps it)
+_GAUSS2D = gaussian2d
+
+
+def use_astropy_models(models):
+    """Evaluate every Gaussian the way the reference does, through astropy objects:
+    ``models.Gaussian2D(amplitude=..., x_mean=..., y_mean=..., x_stddev=...,
+    y_stddev=..., theta=...)(x, y)`` (apf_step2.py:98-102) -- the object construction
+    and parameter validation the reference pays for twice per source per proposal
+    (about 85 % of its build_2d_gaussian).  The values are those of
+    ``gaussian2d`` (astropy's call is its ``evaluate``); only the cost differs.  Used by
+    oracle/astropy_timing.py (/opt/conda python3.9 + astropy 4.3.1) for the CPU
+    baseline of the reference's own loop cost on the GPU box's cores."""
+    global _GAUSS2D
+
+    def g(x, y, amplitude, x_mean, y_mean, x_stddev, y_stddev, theta):
+        return models.Gaussian2D(amplitude=amplitude, x_mean=x_mean, y_mean=y_mean,
+                                 x_stddev=x_stddev, y_stddev=y_stddev, theta=theta)(x, y)
+    _GAUSS2D = g
+
+
 def grid(n: int):
     """``y, x = np.mgrid[:ysize, :xsize]`` (apf_step2.py:94) for a square n x n image
     (the reference is square-only: apf_step2.py:237 swaps the axes)."""
@@ -97,10 +118,10 @@ def build_2d_gaussian(yx, xc, yc, dx, dy, total_amplitude, amplituderatio, backg
     total_amplitude = total_amplitude - background                      # :95
     wide_amplitude = total_amplitude * amplituderatio                   # :96
     narrow_amplitude = total_amplitude - wide_amplitude                 # :97
-    narrow = gaussian2d(x, y, narrow_amplitude, xc, yc, narrow_sigma_x,
-                        narrow_sigma_y, narrow_theta)                   # :98-99
-    wide = gaussian2d(x, y, wide_amplitude, xc + dx, yc + dy, wide_sigma_x,
-                      wide_sigma_y, wide_theta)                         # :100-101
+    narrow = _GAUSS2D(x, y, narrow_amplitude, xc, yc, narrow_sigma_x,
+                      narrow_sigma_y, narrow_theta)                     # :98-99
+    wide = _GAUSS2D(x, y, wide_amplitude, xc + dx, yc + dy, wide_sigma_x,
+                    wide_sigma_y, wide_theta)                           # :100-101
     return wide + narrow                                                # :102
 
 

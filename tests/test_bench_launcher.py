@@ -126,6 +126,11 @@ def test_config0_line_beside_one_core():
     assert 0 < cb["reference_over_port"] < 1
     assert cb["reference_value_derived"] == pytest.approx(cb["value"] * cb["reference_over_port"])
     assert d["gpu_over_reference"] == pytest.approx(d["value"] / cb["reference_value_derived"])
+    # the reference's loop cost measured here: the astropy-object oracle on one core
+    if os.path.exists("/opt/conda/bin/python3.9"):
+        rl = cb["reference_like"]
+        assert rl["cores"] == 1 and "1000 iterations" in rl["sample"] and rl["value"] > 0
+        assert d["gpu_over_reference_like"] == pytest.approx(d["value"] / rl["value"])
 
 
 def test_per_config_defaults_cover_the_survey_runs():

@@ -137,3 +137,25 @@ def test_oracle_long_chain_matches_reference(golden, name, walker):
     w = ora.Walker(dm, err, g["p_init"], int(g["seeds"][walker]), nsrc)
     chain, _ = w.run(L)
     np.testing.assert_allclose(chain, g["traj_params"][walker, :L], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("name,walker,iters", [("c64_long", 2, 800), ("c128_3_long", 0, 250),
+                                               ("c32_long", 1, 600)])
+def test_astropy_oracle_is_the_reference(name, walker, iters):
+    """oracle/astropy_timing.py (bench.py's reference-cost CPU baseline): the oracle's
+    walker with astropy Gaussian2D objects per proposal, under the image's python3.9 /
+    numpy 1.26 / astropy 4.3.1, gives the reference's own chains BIT FOR BIT (the long
+    fixtures were written by the reference's lines under the same interpreter)."""
+    import json
+    import os
+    import subprocess
+    py = "/opt/conda/bin/python3.9"
+    if not os.path.exists(py):
+        pytest.skip("no /opt/conda python3.9")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([py, os.path.join(repo, "oracle", "astropy_timing.py"), "--check",
+                        os.path.join(repo, "tests", "golden", f"{name}.npz"), str(walker),
+                        str(iters)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["rows"] == iters and d["bit_equal"] is True
