@@ -250,8 +250,14 @@ def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | No
     res = []
     try:
         # every process imported astropy and warmed up: start their loops together
-        if any(p.stdout.readline().strip() != "ready" for p in ps):
-            return None
+        # (a process that does not get there within 180 s voids the measurement)
+        import select
+        deadline = time.monotonic() + 180.0
+        for p in ps:
+            if not select.select([p.stdout], [], [], max(0.0, deadline - time.monotonic()))[0]:
+                return None
+            if p.stdout.readline().strip() != "ready":
+                return None
         for p in ps:
             p.stdin.write("go\n")
             p.stdin.flush()
