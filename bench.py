@@ -266,6 +266,8 @@ def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | No
             if p.returncode != 0:
                 return None
             res.append(json.loads(out.strip().splitlines()[-1]))
+    except (subprocess.TimeoutExpired, OSError, ValueError, IndexError):
+        return None              # no reference-cost figure rather than no bench line
     finally:
         for p in ps:
             if p.poll() is None:
