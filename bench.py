@@ -474,7 +474,10 @@ def main():
                     help="timed steps (default: the config's, DEFAULTS)")
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps first (default: the config's, DEFAULTS)")
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json config index: 0 one walker 32x32, 1 4,096 walkers, "
+                         "2 65,536 walkers per GPU (default), 3 = 2 over 8 GPUs, 4 3-source "
+                         "128x128 (16,384 per GPU)")
     ap.add_argument("--walkers", type=int, default=0, help="override walkers per GPU")
     ap.add_argument("--iters", type=int, default=None,
                     help="Gibbs iterations per step (default: the config's, DEFAULTS)")
