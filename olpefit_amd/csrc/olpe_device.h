@@ -1581,7 +1581,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // counted waits stay correct because vector memory operations retire in order.
 
 // (Windowed rings without barriers -- four and five slots of 16-row phases -- ran 6 %
-// and 9 % slower; DESIGN.md §7.2, removed in round 4.)
+// and 9 % slower; DESIGN_HISTORY.md §7.2, removed in round 4.)
 template <int WAVES> struct LdsRing {
   static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
   static constexpr int SLOTS = 2, AHEAD = 1;              // ring slots; DMA lead in phases
