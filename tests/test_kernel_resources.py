@@ -92,3 +92,34 @@ def test_other_bench_configs_have_no_scratch(usage):
     for args in [(3, 128, False, 12, True), (3, 128, False, 4, True), (3, 64, True, 12, True)]:
         k = _kernel(usage, *args)
         assert k["scratch_insts"] == 0 and k["VGPRs Spill"] == 0, (args, k)
+
+
+def test_moment_fold_kernels_have_no_scratch():
+    """The HBM-bound fold kernels (olpe_moments.hip): the one-wave-per-
+    walker fold keeps 16 loads in flight per lane in registers -- no spill, and few
+    enough VGPRs that the 4-wave blocks fill the CUs."""
+    if not (os.path.exists(HIPCC) or shutil.which("hipcc")):
+        pytest.skip("hipcc not available")
+    from olpefit_amd import build
+    flags = [f for f in build.FLAGS if f not in ("-shared", "-fPIC", "-Wall",
+                                                  "-Wno-unused-function")]
+    cmd = [HIPCC, *flags, "--cuda-device-only", "-c", "-o", os.devnull,
+           os.path.join(REPO, "olpefit_amd", "csrc", "olpe_moments.hip"),
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600).stderr
+    res, name = {}, None
+    for line in out.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            res[name] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs|ScratchSize \[bytes/lane\]|VGPRs Spill): (\d+)", line)
+        if m and name:
+            res[name][m.group(1)] = int(m.group(2))
+    for kern in ("fold_rows_kernel", "fold_cols_kernel"):
+        hits = [v for k, v in res.items() if kern in k]
+        assert hits, kern
+        v = hits[0]
+        assert v["ScratchSize [bytes/lane]"] == 0 and v["VGPRs Spill"] == 0, (kern, v)
+        assert v["VGPRs"] <= 128, (kern, v)
