@@ -284,6 +284,29 @@ def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | No
                       "(tests/test_oracle_golden.py::test_astropy_oracle_is_the_reference)"}
 
 
+def csv_emission(s, nw: int, threads: int) -> dict:
+    """Write the last launch's chain rows of walkers [0, nw) as ``{w}_finalarray_mpi.csv``
+    (the all-NaN seed row, then the rows; csv.writer's bytes, apf_step2.py:342-360)
+    into a temporary directory with the native threaded writer; returns the time."""
+    import shutil
+    import tempfile
+    from olpefit_amd import pipeline
+    rows = s.chain()[:nw]
+    d = tempfile.mkdtemp(prefix="olpe_csv_")
+    try:
+        paths = [os.path.join(d, f"{w}_finalarray_mpi.csv") for w in range(nw)]
+        t = time.perf_counter()
+        pipeline.write_chain_csvs(paths, rows, nan_row=True, threads=threads)
+        dt = time.perf_counter() - t
+        nbytes = sum(os.path.getsize(p) for p in paths)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"files": nw, "rows_per_file": int(rows.shape[1]) + 1, "bytes": nbytes,
+            "ms": dt * 1e3, "mb_per_s": nbytes / dt / 1e6, "threads": threads,
+            "note": "outside the timed region (SURVEY.md 8(d)); the native csv.writer-exact "
+                    "writer (olpe_csv_write_chains), files created in a temporary directory"}
+
+
 def reference_ratio(n: int, nsrc: int, path: str):
     """The reference's own apf_step2 loop against the port on one core of the build
     container (tests/golden/time_reference.py --json; the reference cannot travel to the
@@ -491,6 +514,8 @@ def main():
                          "core (default: about 12 s of CPU work: 96,000 at 64x64, scaled by "
                          "64^2/n^2 otherwise)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-csv", action="store_true",
+                    help="skip the (untimed) CSV-emission figure of the last launch's rows")
     ap.add_argument("--no-reference-like", action="store_true",
                     help="skip the astropy-object (reference-cost) CPU baseline")
     ap.add_argument("--cpu-steps-ref", type=int, default=None,
@@ -834,6 +859,11 @@ def main():
             "gr_rc_max": max(rc) if all(np.isfinite(rc)) else None,
             "acceptance": sum(summ[k]["accepts"] for k in names[:-1])
             / sum(summ[k]["tries"] for k in names[:-1])}
+    if world == 1 and not args.no_csv and getattr(s, "_nrec", 0):
+        # "timing excludes CSV emission, which is reported separately" --
+        # the last launch's rows of (up to) 4,096 walkers written as the reference's
+        # per-walker chain files by the native writer, outside the timed region
+        out["csv_emission"] = csv_emission(s, min(s.W, 4096), host_cpus()[0])
     value = out["value"]
     if not args.no_cpu_baseline and world == 1:
         cpu_steps = args.cpu_steps or max(4000, 96000 * 64 * 64 // (n * n))

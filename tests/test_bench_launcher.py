@@ -240,3 +240,13 @@ def test_config3_names_its_part():
     assert r.returncode == 0, r.stderr
     w = _line(r)["config"]["workload"]
     assert w.startswith("configs[3]'s per-GPU shards on 2 GPUs") and "--gpus 8" in w
+
+
+def test_csv_emission_reported_outside_the_timed_region():
+    """CSV emission is timed separately -- the last launch's rows of up to
+    4,096 walkers written as the reference's chain files (stub rows here)."""
+    r = _run([])
+    assert r.returncode == 0, r.stderr
+    c = _line(r)["csv_emission"]
+    assert c["files"] == WPG and c["rows_per_file"] == ITERS // STRIDE + 1
+    assert c["bytes"] > 0 and c["ms"] > 0 and c["mb_per_s"] > 0
