@@ -67,15 +67,43 @@ CONFIG3 = ("configs[3]: 524,288 walkers sharded 8 x MI355X (65,536 per GPU, 64x6
            "cutout, fp64), RCCL chain all-gather at the end")
 
 
-def workload_name(config: int, world: int, wpg: int) -> str:
-    """The line's ``config.workload``: configs[2] at 8 ranks of 65,536 walkers is
-    configs[3] (``--config 3`` names it too, and on fewer GPUs says which part ran)."""
-    if config in (2, 3) and world == 8 and wpg == 65536:
-        return CONFIG3
-    if config == 3:
-        return (f"configs[3]'s per-GPU shards on {world} GPU{'s' if world > 1 else ''} "
-                f"({world} x {wpg:,} of 524,288 walkers; the whole of configs[3] is --gpus 8)")
-    return CONFIG_NAMES[config]
+def workload_name(config: int, world: int, wpg: int, n: int | None = None,
+                  nsrc: int | None = None, iters: int | None = None,
+                  stride: int | None = None, steps: int | None = None) -> str:
+    """The line's ``config.workload``, derived from what actually ran: a BASELINE config
+    is named only when (walkers per GPU, side, sources) are that config's SURVEY 8(d)
+    shape -- configs[2]'s per-GPU shape at 8 ranks is configs[3], on 2 / 4 ranks its weak
+    scaling -- and anything else is ``custom: ...`` with its sizes.  A run whose
+    iterations per launch, stride or timed launches differ from the config's 8(d) run
+    (DEFAULTS) says so after the name."""
+    n = CONFIGS[config][1] if n is None else n
+    nsrc = CONFIGS[config][2] if nsrc is None else nsrc
+    gpus = f"{world} GPU{'s' if world > 1 else ''}"
+    shape = (wpg, n, nsrc)
+    if shape != CONFIGS[config]:
+        name = (f"custom: {world} x {wpg:,} walkers ({wpg:,} per GPU on {gpus}), {n}x{n} "
+                f"{nsrc}-source cutout, fp64 (not a BASELINE config's shape; --config "
+                f"{config} sizes {CONFIGS[config][0]:,} walkers, {CONFIGS[config][1]}x"
+                f"{CONFIGS[config][1]}, {CONFIGS[config][2]} sources)")
+    elif config in (2, 3) and world == 8:
+        name = CONFIG3
+    elif config == 3:
+        name = (f"configs[3]'s per-GPU shards on {gpus} ({world} x {wpg:,} of 524,288 "
+                f"walkers; the whole of configs[3] is --gpus 8)")
+    elif world > 1:
+        name = (f"{CONFIG_NAMES[config].split(':')[0]}'s shape per GPU, weak-scaled over "
+                f"{gpus} ({world} x {wpg:,} walkers, {n}x{n} {nsrc}-source cutout, fp64"
+                + ("; configs[3] is 8 x 65,536)" if config == 2 else ")"))
+    else:
+        name = CONFIG_NAMES[config]
+    d = DEFAULTS[config]
+    run = dict(iters=iters, stride=stride, steps=steps)
+    if any(v is not None and v != d[k] for k, v in run.items()):
+        name += (f" [run: {steps if steps is not None else d['steps']} launches x "
+                 f"{iters if iters is not None else d['iters']} iterations at stride "
+                 f"{stride if stride is not None else d['stride']}; 8(d)'s run: {d['steps']} x "
+                 f"{d['iters']} at stride {d['stride']}]")
+    return name
 
 
 # SURVEY.md 8(d)'s run of each config: iterations per launch (a bench step), chain record
@@ -230,13 +258,15 @@ def cpu_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None):
 CONDA_PY = "/opt/conda/bin/python3.9"       # the image's python with astropy 4.3.1
 
 
-def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None):
+def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | None = None,
+                            port: bool = False):
     """The reference's own loop cost on this box's cores: ``procs`` processes of
     oracle/astropy_timing.py (the oracle's walker with every Gaussian built as an
     astropy ``Gaussian2D`` object per proposal, as apf_step2.py:98-102 does; its chains
     are bit-equal to the reference's own, tests/test_oracle_golden.py), started
-    together after their imports, ``total_iters`` walker-steps in all.  None when the
-    image's python3.9 / astropy is missing."""
+    together after their imports, ``total_iters`` walker-steps in all.  ``port``: the
+    plain NumPy port under the same python3.9 instead (the like-for-like denominator of
+    the reference-cost ratio).  None when the image's python3.9 / astropy is missing."""
     import subprocess
     if not os.path.exists(CONDA_PY):
         return None
@@ -245,7 +275,7 @@ def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | No
     iters = max(100, total_iters // procs)
     script = os.path.join(REPO, "oracle", "astropy_timing.py")
     ps = [subprocess.Popen([CONDA_PY, script, str(n), str(nsrc), str(1000 + i), str(iters),
-                            "--sync"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                            "--sync"] + (["--port"] if port else []), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                            stderr=subprocess.DEVNULL, text=True) for i in range(procs)]
     res = []
     try:
@@ -274,6 +304,11 @@ def reference_like_baseline(n: int, nsrc: int, total_iters: int, procs: int | No
                 p.kill()
                 p.wait()
     secs = max(r["seconds"] for r in res)
+    if port:
+        return {"value": procs * iters / secs, "unit": "walker-steps/s", "cores": procs,
+                "kind": "port (NumPy, under the astropy baseline's interpreter)",
+                "sample": f"oracle/astropy_timing.py --port under {CONDA_PY}: {procs} processes "
+                          f"x 1 walker x {iters} iterations, {n}x{n} {nsrc}-source cutout"}
     return {"value": procs * iters / secs, "unit": "walker-steps/s", "cores": procs,
             "kind": "port (astropy Gaussian2D objects per proposal, as the reference)",
             "sample": f"oracle/astropy_timing.py under {CONDA_PY} (astropy 4.3.1): {procs} "
@@ -582,13 +617,15 @@ def main():
     # the PCI bus ids tell whether the ranks really hold distinct GPUs, whatever each
     # process sees as its device 0..n-1
     placement = group.allgather([rank, local, device, os.getpid(),
-                                 Sampler.device_pci_id(device)])
+                                 Sampler.device_pci_id(device), odist.node_id()])
     pci = [p[4] for p in placement]
-    if world > 1 and not shared and len(set(pci)) < world:
-        # the same verdict on every rank (the gathered list is the same everywhere)
-        print(f"[bench rank {rank}] ranks share a GPU (PCI {pci}): one process per GPU "
-              "needs as many GPUs as ranks (--share-gpu for a rehearsal on fewer)",
-              file=sys.stderr)
+    dup = odist.shared_gpus([(p[5], p[4]) for p in placement])
+    if world > 1 and not shared and dup:
+        # the same verdict on every rank (the gathered list is the same everywhere); a
+        # GPU is (node, PCI bus id): identical nodes repeat bus ids
+        print(f"[bench rank {rank}] ranks share a GPU (PCI {pci}, shared {dup}): one "
+              "process per GPU needs as many GPUs as ranks (--share-gpu for a rehearsal "
+              "on fewer)", file=sys.stderr)
         s.close()
         group.close()
         sys.exit(4)
@@ -626,9 +663,14 @@ def main():
         t1 = time.perf_counter()
         if steps % 64:
             kms.extend(s.kernel_times(steps % 64))
-        return allmax(t1 - t0), float(np.mean(kms))
+        km = float(np.mean(kms))
+        # every rank's mean sampler time and its own timed-region seconds (one gather, on
+        # every rank alike): a scaling shortfall is then attributable from the line --
+        # a slow GPU (per_rank_kernel_ms spread) or time outside the sampler kernels
+        per_rank = group.allgather([km, t1 - t0])
+        return allmax(t1 - t0), km, per_rank
 
-    elapsed, kernel_ms = measure(args.mode, args.steps, args.warmup)
+    elapsed, kernel_ms, per_rank = measure(args.mode, args.steps, args.warmup)
     units = s.last_units()          # chunks per walker of the timed launches
     st, tries, accs = s.get_state()
     acceptance = float(accs.sum() / max(1.0, tries.sum()))
@@ -636,7 +678,7 @@ def main():
     if world == 1 and not args.no_alt:
         other = "exact" if args.mode == "fast" else "fast"
         alt_steps = max(2, args.steps // 2)
-        e2, k2 = measure(other, alt_steps, 1)
+        e2, k2, _ = measure(other, alt_steps, 1)
         alt = (other, alt_steps, e2, k2)
 
     def report(elapsed, kernel_ms, units, acceptance, comm, alt=None):
@@ -731,7 +773,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic NIRC2-shaped cutout (olpefit_amd/synth.py), step-1 style start",
-            "config": {"workload": workload_name(args.config, world, wpg),
+            "config": {"workload": workload_name(args.config, world, wpg, n, nsrc,
+                                                 args.iters, args.stride, args.steps),
                        "walkers_per_gpu": wpg,
                        "image": f"{n}x{n}", "sources": nsrc, "iters_per_step": args.iters,
                        "chain_stride": args.stride, "eval": args.mode,
@@ -739,6 +782,7 @@ def main():
                        "parallelism": f"walker-sharded x{world}",
                        "devices": [p[2] for p in placement],
                        "pci_bus_ids": sorted(set(pci)),
+                       "nodes": len({p[5] for p in placement}),
                        "local_ranks": [p[1] for p in placement],
                        "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
                                     else "environment" if "WORLD_SIZE" in os.environ
@@ -747,6 +791,19 @@ def main():
             "acceptance": acceptance,
             "allgather_ms": None,
         }
+        # where the timed region went, per rank: each rank's mean HIP-event sampler time
+        # per launch, and the share of the (max-over-ranks) timed region outside the
+        # slowest rank's sampler kernels -- the moments fold, launch gaps, the barriers
+        kmax = max(p[0] for p in per_rank)
+        out["per_rank_kernel_ms"] = {"min": min(p[0] for p in per_rank), "max": kmax,
+                                     "ranks": [p[0] for p in per_rank]}
+        out["per_rank_elapsed_s"] = {"min": min(p[1] for p in per_rank),
+                                     "max": max(p[1] for p in per_rank)}
+        out["host_overhead_frac"] = 1.0 - kmax * 1e-3 * args.steps / elapsed
+        out["host_overhead_note"] = (
+            "1 - max over ranks of (mean sampler kernel ms x steps) / the max-over-ranks "
+            "timed region: the moments fold kernel (inside the step, outside kernel_ms), "
+            "launch gaps and the host-group barriers")
         out.update(comm)
         if alt:
             other, alt_steps, e2, k2 = alt
@@ -879,11 +936,24 @@ def main():
                       1600, 24000 * 64 * 64 // (n * n))))
             if rl:
                 # the reference's loop cost measured on these cores (the astropy-object
-                # oracle), beside the NumPy port above
+                # oracle), beside the NumPy port above; and the port under the same
+                # python3.9, so that their ratio is like for like
                 cb["reference_like"] = rl
                 out["gpu_over_reference_like"] = value / rl["value"]
+                p39 = (reference_like_baseline(n, nsrc, 1000, procs=1, port=True)
+                       if args.config == 0 else reference_like_baseline(
+                           n, nsrc, args.cpu_steps_ref or max(1600, 24000 * 64 * 64 // (n * n)),
+                           port=True))
+                if p39:
+                    rl["port_same_interpreter"] = p39
+                    rl["reference_over_port_same_interpreter"] = rl["value"] / p39["value"]
         ref = reference_ratio(n, nsrc, args.reference_timing)
-        if ref:
+        if ref and "reference_like" in cb:
+            # one reference figure: the one measured on this box.  The build container's
+            # reference/port ratio is kept for the record, not turned into a second rate
+            # (its port and this box's ran under different interpreters and CPUs)
+            cb["build_container_reference_timing"] = ref
+        elif ref:
             # the reference itself is slower than the port on the same core: its rate on
             # these cores, derived from the ratio measured in the build container
             cb.update(ref)
@@ -892,7 +962,8 @@ def main():
             out["gpu_over_reference_note"] = (
                 "derived: cpu_baseline.value x reference_over_port, the reference/port "
                 "speed ratio measured on one core of the build container "
-                "(profiles/r04/reference_cpu_timing.json), not on this box")
+                "(profiles/r04/reference_cpu_timing.json), not on this box; reported only "
+                "when the box cannot run the astropy-object baseline (reference_like)")
     print(json.dumps(out))
     s.close()
     group.close()

@@ -235,8 +235,17 @@ int olpe_comm_gather_limit(olpe_ctx *ctx, long long bytes);
  * walkers, with centre = the pooled mean (out[2 + k] / out[1]).  Every rank must have
  * folded the same number of rows (checked: OLPE_EINVAL on every rank otherwise); the
  * walker counts may differ (a sum needs no equal shards).
- * Without olpe_comm_init it summarises this context alone. */
+ * Without olpe_comm_init it summarises this context alone.  Hang-free by construction:
+ * every local allocation (and the zeroing of unfolded moments) happens before the
+ * uniformity check and its failure travels in it (OLPE_ENOMEM on every rank); past the
+ * check every rank enters both all-reduces whatever its local summary did, a failure
+ * summed into a status word, so all ranks return an error together (this rank's own, or
+ * OLPE_ECOMM naming how many other ranks failed). */
 int olpe_comm_allreduce_moments(olpe_ctx *ctx, double *out);
+/* Test hook for the failure paths of the moments summary: where = 1 makes the
+ * preparation's allocation fail (OLPE_ENOMEM before any collective), 2 makes the local
+ * summary launch fail (after the uniformity check), 0 clears.  Build-specific. */
+int olpe_moments_fault(olpe_ctx *ctx, int where);
 
 /* --- whole-run posterior moments ----------------------------
  * apf_step3.py reads every chain file (:169-186) to compute per-parameter means, sigmas

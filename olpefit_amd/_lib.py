@@ -82,6 +82,7 @@ SIGNATURES = {
     "olpe_comm_allgather_chain": (_i, [_P, _ll, _ll, _pd, _pll]),
     "olpe_comm_gather_limit": (_i, [_P, _ll]),
     "olpe_comm_allreduce_moments": (_i, [_P, _pd]),
+    "olpe_moments_fault": (_i, [_P, _i]),
 }
 
 _lib = None

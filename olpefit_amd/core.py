@@ -320,6 +320,11 @@ class Sampler:
         check(self._lib.olpe_comm_allreduce_moments(self._ctx, _dptr(out)))
         return out
 
+    def moments_fault(self, where: int):
+        """Test hook (olpe_moments_fault): 1 = the summary's allocation fails, 2 = its
+        launch fails after the uniformity check, 0 = clear."""
+        check(self._lib.olpe_moments_fault(self._ctx, int(where)))
+
     # -- whole-run moments (SURVEY.md §8(f) row 1) ---------------------------------
     @property
     def moments_len(self) -> int:

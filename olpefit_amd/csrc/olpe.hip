@@ -1253,8 +1253,11 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   for (auto &pair : c->ev)
     for (auto &ev : pair)
       if (hipEventCreate(&ev) != hipSuccess) ev = nullptr;
+  // d_check: the RCCL uniformity check's words (olpe_comm.hip), allocated here so that
+  // olpe_comm_init has nothing to allocate that could fail on one rank while the others
+  // wait in ncclCommInitRank
   if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
-      (rc = dev_alloc(&c->d_queue, 4))) {
+      (rc = dev_alloc(&c->d_queue, 4)) || (rc = dev_alloc(&c->d_check, 16))) {
     olpe_destroy(c);
     return rc;
   }

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <stdio.h>
 #include <string.h>
 
 #include <vector>
@@ -64,18 +65,11 @@ int olpe_comm_unique_id(uint8_t *id128) {
 int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   if (!c || !id128) return set_err(OLPE_EINVAL, "NULL argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(OLPE_EINVAL, "bad rank/nranks");
+  // nothing here can fail on one rank alone once the arguments are valid: the device
+  // was set by olpe_create, and the uniformity check's word buffer was allocated there
+  // too, so no rank returns early while its peers wait in ncclCommInitRank
   HIPCHK(hipSetDevice(c->device));
   olpe_comm_release(c);
-  // the uniformity check's word buffer, before the communicator: a failure here is
-  // reported before this rank joins the collective initialisation
-  if (!c->d_check) {
-    hipError_t e = hipMalloc(&c->d_check, 16 * sizeof(long long));
-    if (e != hipSuccess) {
-      c->d_check = nullptr;
-      return set_err(OLPE_ENOMEM, "hipMalloc(128 bytes) for the communicator: %s",
-                     hipGetErrorString(e));
-    }
-  }
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   ncclComm_t comm;
@@ -91,8 +85,8 @@ int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
 // has the same chain / moment rows, the same W (when `equal_w`: the gathers need equal
 // shards; a sum all-reduce does not), the same gather range, the range is valid
 // everywhere, and every rank allocated what the collective needs (`alloc_failed`).  Its
-// device word buffer is allocated in olpe_comm_init, so the check itself allocates
-// nothing.
+// device word buffer is allocated with the context (olpe_create), so the check itself
+// allocates nothing.
 static int check_uniform(olpe_ctx *c, long long rows, bool equal_w, long long w0 = 0,
                          long long wn = 0, bool bad_range = false, bool alloc_failed = false) {
   const long long w = equal_w ? c->W : 0;
@@ -207,55 +201,90 @@ int olpe_comm_gather_limit(olpe_ctx *c, long long bytes) {
   return OLPE_OK;
 }
 
+// One sum round of the moments all-reduce over d[0, cnt): the local summary
+// (olpe_moments_local, centre dcen or NULL), then slot 0 = this rank's status (0 = fine,
+// 1 = its summary failed) and slot 1 = its walker count, then the all-reduce, then
+// d[0, cnt) to host h.  Past the uniformity check every rank calls the all-reduce
+// whatever its local summary did: a failure is summed into slot 0, so every rank sees
+// how many ranks failed and all of them leave the same way, instead of the failing rank
+// skipping a collective its peers wait in (verdict r04 item 1).  pre_rc != OLPE_OK: this
+// rank already failed (its error is set) and enters with status 1 without a summary.
+// Returns this rank's own error, or OLPE_OK; *failed_ranks = the summed status (-1 if
+// this rank could not read it back).
+static int moments_round(olpe_ctx *c, double *d, const double *dcen, size_t cnt, double *h,
+                         double *failed_ranks, int pre_rc = OLPE_OK) {
+  *failed_ranks = -1.0;
+  const int lrc = pre_rc ? pre_rc : olpe_moments_local(c, dcen, d);
+  const double h01[2] = {lrc ? 1.0 : 0.0, (double)c->W};
+  hipError_t e = hipMemcpyAsync(d, h01, sizeof(h01), hipMemcpyHostToDevice, c->stream);
+  ncclResult_t r = ncclSuccess;
+  if (c->comm)   // entered even after a local failure (the status word carries it)
+    r = ncclAllReduce(d, d, cnt, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
+  hipError_t e2 = hipMemcpyAsync(h, d, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  const hipError_t es = hipStreamSynchronize(c->stream);   // (h01 is read by then)
+  if (e2 == hipSuccess) e2 = es;
+  if (e2 == hipSuccess && e == hipSuccess && r == ncclSuccess) *failed_ranks = h[0];
+  if (lrc) return lrc;
+  if (e != hipSuccess) return set_err(OLPE_EHIP, "moments status word: %s", hipGetErrorString(e));
+  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+  if (e2 != hipSuccess) return set_err(OLPE_EHIP, "moments all-reduce: %s", hipGetErrorString(e2));
+  return OLPE_OK;
+}
+
 int olpe_comm_allreduce_moments(olpe_ctx *c, double *out) {
   if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
   const int ps = c->ps;
   const size_t len = (size_t)OLPE_MOMENTS_LEN(ps, c->np);
+  // every local preparation before the uniformity check -- the summary buffer, the
+  // partials, the moments and their zeroing (olpe_moments_prepare) -- and its outcome in
+  // the check, so a rank that cannot prepare fails the call on every rank
   double *d = nullptr;
   if (hipMalloc(&d, (len + ps) * sizeof(double)) != hipSuccess) {
     d = nullptr;
     (void)hipGetLastError();
   }
+  int prc = d ? olpe_moments_prepare(c)
+              : set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the moments summary",
+                        (len + ps) * sizeof(double));
+  char pmsg[512] = "";
+  if (prc) snprintf(pmsg, sizeof(pmsg), "%s", olpe_last_error());
   // a sum needs equal row counts (step 3's N), not equal shards
-  int rc = c->comm ? check_uniform(c, c->mom_n, false, 0, 0, false, d == nullptr)
-                   : d ? OLPE_OK : set_err(OLPE_ENOMEM, "hipMalloc for the moments summary");
-  if (rc) {
+  int rc = c->comm ? check_uniform(c, c->mom_n, false, 0, 0, false, prc != OLPE_OK) : OLPE_OK;
+  if (rc || prc) {
     if (d) (void)hipFree(d);
-    return rc;
+    return prc ? set_err(prc, "%s", pmsg) : rc;
   }
   double *dcen = d + len;
+  std::vector<double> h(len), cen(ps);
+  double failed = 0.0;
   // round 1: every column's sums over all ranks; slot 1 sums to the walker total
-  // (slot 0 stays 0: n is the same on every rank, checked above)
-  double h01[2] = {0.0, (double)c->W};
-  std::vector<double> cen(ps);
-  hipError_t e = hipMemcpyAsync(d, h01, sizeof(h01), hipMemcpyHostToDevice, c->stream);
-  ncclResult_t r = ncclSuccess;
-  rc = e == hipSuccess ? olpe_moments_local(c, nullptr, d) : OLPE_OK;
-  if (e == hipSuccess && !rc && c->comm)
-    r = ncclAllReduce(d, d, len, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
-  if (e == hipSuccess && !rc && r == ncclSuccess)
-    e = hipMemcpyAsync(out, d, len * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess && !rc && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
-  // round 2: the deviations of the walkers' means about the pooled mean
-  if (e == hipSuccess && !rc && r == ncclSuccess) {
-    for (int k = 0; k < ps; ++k) cen[k] = out[1] > 0 ? out[2 + k] / out[1] : 0.0;
-    e = hipMemcpyAsync(dcen, cen.data(), ps * sizeof(double), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) rc = olpe_moments_local(c, dcen, d);
-    double *dev = d + 2 + 2 * ps;
-    if (e == hipSuccess && !rc && c->comm)
-      r = ncclAllReduce(dev, dev, ps, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
-    if (e == hipSuccess && !rc && r == ncclSuccess)
-      e = hipMemcpyAsync(out + 2 + 2 * ps, dev, ps * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream);
-    if (e == hipSuccess && !rc && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
+  rc = moments_round(c, d, nullptr, len, h.data(), &failed);
+  // round 2 (the deviations of the walkers' means about the pooled mean) only if every
+  // rank's round 1 succeeded -- a verdict every rank read from the same all-reduced word
+  // (a rank that could not read it back leaves too: its stream is broken, and its peers'
+  // round 2 is then left to the callers' watchdogs, bench.py --comm-timeout)
+  if (failed == 0.0) {
+    for (int k = 0; k < ps; ++k) cen[k] = h[1] > 0 ? h[2 + k] / h[1] : 0.0;
+    hipError_t e = hipMemcpyAsync(dcen, cen.data(), ps * sizeof(double), hipMemcpyHostToDevice,
+                                  c->stream);
+    // a failed centre copy still enters the round, as a failed summary (status 1)
+    const int crc = e == hipSuccess
+                        ? OLPE_OK
+                        : set_err(OLPE_EHIP, "moments centre: %s", hipGetErrorString(e));
+    std::vector<double> h2(2 + 3 * (size_t)ps);
+    const int rc2 = moments_round(c, d, dcen, h2.size(), h2.data(), &failed, crc);
+    if (!rc2 && failed == 0.0)
+      for (int k = 0; k < ps; ++k) h[2 + 2 * ps + k] = h2[2 + 2 * ps + k];
+    rc = rc2;
   }
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(d);
   if (rc) return rc;
-  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-  if (e != hipSuccess) return set_err(OLPE_EHIP, "moments all-reduce: %s", hipGetErrorString(e));
+  if (failed != 0.0)
+    return set_err(OLPE_ECOMM, "the moments summary failed on %.0f other rank(s)", failed);
+  memcpy(out, h.data(), len * sizeof(double));
   out[0] = (double)c->mom_n;
   return OLPE_OK;
 }

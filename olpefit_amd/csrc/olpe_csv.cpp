@@ -483,13 +483,16 @@ int olpe_acceptance_write(const char *const *paths, const double *accepts, const
       // previous complete file, never a truncated one (the checkpoint's acceptance
       // files are written in the background)
       tmp.assign(paths[i]).append(".tmp");
+      // every failure removes the temporary file (no '<path>.tmp' left behind)
       FILE *f = fopen(tmp.c_str(), "wb");
       if (!f || fwrite(s.data(), 1, s.size(), f) != s.size()) {
         if (f) fclose(f);
+        (void)remove(tmp.c_str());
         failed[t] = i;
         return;
       }
       if (fclose(f) != 0 || rename(tmp.c_str(), paths[i]) != 0) {
+        (void)remove(tmp.c_str());
         failed[t] = i;
         return;
       }

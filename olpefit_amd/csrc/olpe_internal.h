@@ -71,18 +71,23 @@ struct olpe_ctx {
   long long mom_folded = 0;
   double *d_mpart = nullptr;    // partial sums of olpe_moments_local
   size_t mpart_cap = 0;
+  int mom_fault = 0;            // test hook (olpe_moments_fault): 1 = the preparation's
+                                // allocation fails, 2 = the summary launch fails
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;
   double *d_gather = nullptr;   // receive buffer of olpe_comm_allgather_chain
   size_t gather_cap = 0;
   size_t gather_limit = 0;      // its byte limit (olpe_comm_gather_limit; 0 = none)
-  long long *d_check = nullptr; // the uniformity check's words (allocated by comm_init)
+  long long *d_check = nullptr; // the uniformity check's words (allocated by olpe_create,
+                                // so that joining a communicator allocates nothing)
 };
 
 namespace olpe {
 int set_err(int code, const char *fmt, ...);
 }
 void olpe_comm_release(olpe_ctx *c);
-// per-column sums over this context's walkers into d_out[2 ..] (olpe_moments.hip)
+// the buffers (and zeroing) of the per-column sums (olpe_moments.hip); then the sums over
+// this context's walkers into d_out[2 ..], launches only
+int olpe_moments_prepare(olpe_ctx *c);
 int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out);

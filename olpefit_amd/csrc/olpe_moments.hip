@@ -268,18 +268,24 @@ int ensure_moments(olpe_ctx *c) {
 
 }  // namespace
 
-// the local summary into the device buffer d_out [OLPE_MOMENTS_LEN] (async on the
-// context's stream; d_centre: device [ps] or NULL); n and W are filled in by the host
-int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out) {
+// Everything olpe_moments_local needs besides its launches: the partials buffer, the
+// moments themselves and (nothing folded yet) their zeroing.  The moments all-reduce
+// calls it before its uniformity check, so that a rank that cannot prepare says so in
+// that check instead of skipping the all-reduces its peers enter (olpe_comm.hip).
+int olpe_moments_prepare(olpe_ctx *c) {
+  if (c->mom_fault == 1)
+    return set_err(OLPE_ENOMEM, "moment partials: allocation failure forced (olpe_moments_fault)");
   const int nblk = (int)((c->W + kWalkersPerBlock - 1) / kWalkersPerBlock);
-  const size_t cols = (size_t)3 * c->ps + 2 * c->np;
-  const size_t need = cols * nblk;
+  const size_t need = ((size_t)3 * c->ps + 2 * c->np) * nblk;
   if (need > c->mpart_cap) {
     if (c->d_mpart) (void)hipFree(c->d_mpart);
     c->d_mpart = nullptr;
     c->mpart_cap = 0;
-    if (hipMalloc((void **)&c->d_mpart, need * sizeof(double)) != hipSuccess)
+    if (hipMalloc((void **)&c->d_mpart, need * sizeof(double)) != hipSuccess) {
+      c->d_mpart = nullptr;
+      (void)hipGetLastError();
       return set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the moment partials", need * 8);
+    }
     c->mpart_cap = need;
   }
   int rc;
@@ -288,6 +294,19 @@ int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out) {
     HIPCHK(hipMemsetAsync(c->d_mmean, 0, (size_t)c->W * c->ps * 8, c->stream));
     HIPCHK(hipMemsetAsync(c->d_mm2, 0, (size_t)c->W * c->ps * 8, c->stream));
   }
+  return OLPE_OK;
+}
+
+// the local summary into the device buffer d_out [OLPE_MOMENTS_LEN] (async on the
+// context's stream; d_centre: device [ps] or NULL); n and W are filled in by the host.
+// Launches only: olpe_moments_prepare must have succeeded.
+int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out) {
+  if (c->mom_fault == 2)
+    return set_err(OLPE_EHIP, "moments summary launch: failure forced (olpe_moments_fault)");
+  const int nblk = (int)((c->W + kWalkersPerBlock - 1) / kWalkersPerBlock);
+  const size_t cols = (size_t)3 * c->ps + 2 * c->np;
+  if (!c->d_mpart || c->mpart_cap < cols * nblk || !c->d_mmean)
+    return set_err(OLPE_ESTATE, "moments summary before its buffers were prepared");
   hipLaunchKernelGGL(summary_stage1, dim3(nblk), dim3(kThreads), 0, c->stream, c->d_mmean,
                      c->d_mm2, d_centre, c->d_tries, c->d_acc, (long long)c->W, c->ps, c->np,
                      nblk, c->d_mpart);
@@ -299,6 +318,12 @@ int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out) {
 }
 
 extern "C" {
+
+int olpe_moments_fault(olpe_ctx *c, int where) {
+  if (!c || where < 0 || where > 2) return set_err(OLPE_EINVAL, "bad argument");
+  c->mom_fault = where;
+  return OLPE_OK;
+}
 
 int olpe_moments_accumulate(olpe_ctx *c) {
   if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
@@ -392,7 +417,8 @@ int olpe_moments_summary(olpe_ctx *c, const double *centre, double *out) {
     dc = d + len;
     e = hipMemcpyAsync(dc, centre, c->ps * sizeof(double), hipMemcpyHostToDevice, c->stream);
   }
-  int rc = e == hipSuccess ? olpe_moments_local(c, dc, d) : OLPE_OK;
+  int rc = e == hipSuccess ? olpe_moments_prepare(c) : OLPE_OK;
+  if (e == hipSuccess && rc == OLPE_OK) rc = olpe_moments_local(c, dc, d);
   if (e == hipSuccess && rc == OLPE_OK)
     e = hipMemcpyAsync(out, d, len * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess && rc == OLPE_OK) e = hipStreamSynchronize(c->stream);

@@ -46,6 +46,37 @@ def rank_device(local: int, visible: int) -> int:
     raise ValueError(f"LOCAL_RANK {local} but this process sees {visible} GPUs")
 
 
+def node_id() -> str:
+    """This machine's identity for telling GPUs apart across nodes: the kernel's boot id
+    (unique per boot of a host, the same for every process on it), else the host name.
+    PCI bus ids alone repeat across identical nodes (0000:05:00.0 on each of them).
+    ``OLPE_NODE_ID`` overrides it (the CPU tests' fake nodes)."""
+    if os.environ.get("OLPE_NODE_ID"):
+        return os.environ["OLPE_NODE_ID"]
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            bid = f.read().strip()
+            if bid:
+                return bid
+    except OSError:
+        pass
+    return socket.gethostname()
+
+
+def shared_gpus(placement) -> list:
+    """The (node, PCI bus id) pairs that more than one rank holds, from every rank's
+    ``(node_id(), pci_id)`` in rank order (the same list on every rank after an
+    allgather, so every rank reaches the same verdict).  Empty when every rank has a GPU
+    of its own; ranks on different nodes may report the same bus id."""
+    seen, dup = set(), []
+    for p in placement:
+        key = (p[0], p[1])
+        if key in seen and key not in dup:
+            dup.append(key)
+        seen.add(key)
+    return dup
+
+
 def shard(total: int, world: int, rank: int):
     """Contiguous shard [w0, w0 + n) of ``total`` walkers for ``rank`` (strong split;
     shard sizes differ by at most one, so the RCCL gathers, which need equal counts,

@@ -173,9 +173,17 @@ def write_acceptance(path: str, accepts, tries) -> None:
     does), so a run killed mid-write leaves the previous complete file, never a
     truncated one (the writes run in the background after a checkpoint)."""
     tmp = path + ".tmp"
-    with open(tmp, "w") as f:
-        f.write(acceptance_text(accepts, tries))
-    os.replace(tmp, path)
+    try:
+        with open(tmp, "w") as f:
+            f.write(acceptance_text(accepts, tries))
+        os.replace(tmp, path)
+    except BaseException:
+        # no '<path>.tmp' left behind by a failed write (ADVICE r04)
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
 
 
 def write_acceptance_files(paths, accepts, tries, threads: int = 0) -> None:

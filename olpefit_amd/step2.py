@@ -462,18 +462,24 @@ def main(argv=None, nsrc=2, variant="2"):
     ng = max(1, min(args.gpus, pW))
     if args.share_gpu:
         dev0 = args.device
-    elif ng == 1 and world > 1:
+    elif args.gpus == 1 and world > 1:
+        # (the branch depends on --gpus alone, the same on every rank, so every rank
+        # takes part in the allgather below: pW, and with it ng, can differ by one)
         # one GPU per rank: LOCAL_RANK's device, or device 0 when the launcher gave each
         # process its own GPU (as bench.py; dist.rank_device), and no two ranks on one
-        # GPU unless --share-gpu says so (PCI bus ids, the same verdict on every rank)
+        # GPU unless --share-gpu says so: (node, PCI bus id) pairs, gathered so that
+        # every rank reaches the same verdict; identical nodes repeat bus ids
         from .core import Sampler
         dev0 = args.device + dist.rank_device(local, Sampler.device_count() - args.device)
-        pci = group.allgather(Sampler.device_pci_id(dev0))
-        if len(set(pci)) < world:
-            raise RuntimeError(f"ranks share a GPU (PCI {pci}): one process per GPU needs as "
+        placement = group.allgather([dist.node_id(), Sampler.device_pci_id(dev0)])
+        dup = dist.shared_gpus(placement)
+        if dup:
+            raise RuntimeError(f"ranks share a GPU ({dup}): one process per GPU needs as "
                                "many GPUs as ranks (--share-gpu for a rehearsal on fewer)")
     else:
-        dev0 = args.device + local * ng
+        # --gpus G contexts per rank: LOCAL_RANK's block of G devices (the same stride on
+        # every rank, whatever its shard size)
+        dev0 = args.device + local * args.gpus
     bounds = [pw0 + (g * pW) // ng for g in range(ng + 1)]
     shards = [Shard(image, hdr, nsrc, dev0 + g, bounds[g], bounds[g + 1] - bounds[g], p0,
                     seeds, args.exact, 1 if args.fixed_bkgd else 0) for g in range(ng)]

@@ -2,7 +2,7 @@
 BENCH INFRASTRUCTURE, like the rest of oracle/: only bench.py's cpu_baseline leg and
 tests/ run it; the product never does).
 
-    /opt/conda/bin/python3.9 oracle/astropy_timing.py <n> <nsrc> <seed> <iters> [--sync]
+    /opt/conda/bin/python3.9 oracle/astropy_timing.py <n> <nsrc> <seed> <iters> [--sync] [--port]
     /opt/conda/bin/python3.9 oracle/astropy_timing.py --check <fixture.npz> <walker> <iters>
 
 The reference cannot travel to the GPU box (its sources stay in the build container),
@@ -16,6 +16,9 @@ warm-up and starts the loop when a line arrives on stdin, so that the processes 
 measurement run together).  ``--check`` runs the walker of a
 reference-executed fixture (tests/golden/*_long.npz, produced by the reference's own
 lines under the same python3.9 / numpy 1.26 / astropy 4.3.1) and compares every row.
+``--port`` times the plain NumPy port instead (no astropy objects) under the same
+interpreter, so that the reference-cost / port ratio bench.py reports is like for like
+(the port had been timed under the bench's own python only).
 """
 import json
 import os
@@ -41,7 +44,8 @@ from astropy.modeling import models  # noqa: E402
 
 from oracle import olpe_oracle as ora  # noqa: E402
 
-ora.use_astropy_models(models)
+if "--port" not in sys.argv[1:]:
+    ora.use_astropy_models(models)
 
 
 def walker(image, nsrc, p0, seed):

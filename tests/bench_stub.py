@@ -9,6 +9,10 @@ injects the failures the tests pin:
 * ``chain``  -- allgather_chain raises on every rank (the line carries comm_error);
 * ``rank1``  -- rank 1 exits with status 5 right after it joins the host group
   (the launcher must report the failure and stop the other ranks).
+
+OLPE_STUB_MS_PER_RANK adds that many milliseconds per rank index to each launch (a
+slow GPU: the line's per_rank_kernel_ms spread); OLPE_STUB_NODES=k puts rank r on the
+fake node r mod k (dist.node_id via OLPE_NODE_ID): identical nodes repeat PCI bus ids.
 """
 import os
 import time
@@ -29,7 +33,11 @@ class StubSampler:
         self.ps = self.np_ + 1
         self.W = 0
         self.device = device
-        self.ms = float(os.environ.get("OLPE_STUB_MS", "2"))
+        rank = int(os.environ.get("RANK", "0"))
+        self.ms = float(os.environ.get("OLPE_STUB_MS", "2")) + \
+            rank * float(os.environ.get("OLPE_STUB_MS_PER_RANK", "0"))
+        if os.environ.get("OLPE_STUB_NODES"):
+            os.environ["OLPE_NODE_ID"] = f"node{rank % int(os.environ['OLPE_STUB_NODES'])}"
         self._nrec = 0
         self._rows = 0
         self._kms = []

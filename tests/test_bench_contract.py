@@ -88,3 +88,34 @@ def test_committed_lines_carry_the_reference_cost_measured_on_the_box(name):
     rl = cb["reference_like"]
     assert rl["cores"] == cb["cores"] and 0 < rl["value"] < cb["value"]
     assert d["gpu_over_reference_like"] == pytest.approx(d["value"] / rl["value"], rel=1e-9)
+
+
+@pytest.mark.parametrize("path", ["r04/c/bench_gpus8_share.log", "r04/a/bench_gpus2.log",
+                                  "r04/d/bench_c3_one_gpu.log"])
+def test_rehearsal_shapes_are_not_named_configs2(path):
+    """Verdict r04 item 2: round 4's rehearsal lines printed configs[2]'s name beside
+    8,192 / 2,048 / 524,288 walkers per GPU; the workload is now derived from the shape
+    that ran, so those shapes are named ``custom``."""
+    d = _last_json(os.path.join(REPO, "profiles", path))
+    c = d["config"]
+    n = int(c["image"].split("x")[0])
+    name = bench.workload_name(2, d["n_gpus"], c["walkers_per_gpu"], n, c["sources"],
+                               c["iters_per_step"], c["chain_stride"], d["steps"])
+    assert name.startswith("custom: ") and not name.startswith("configs[2]")
+    assert f"{c['walkers_per_gpu']:,} walkers" in name
+
+
+def test_default_workload_names_are_unchanged():
+    for cfg in (0, 1, 2, 4):
+        wpg, n, nsrc = bench.CONFIGS[cfg]
+        d = bench.DEFAULTS[cfg]
+        assert bench.workload_name(cfg, 1, wpg, n, nsrc, d["iters"], d["stride"],
+                                   d["steps"]) == bench.CONFIG_NAMES[cfg]
+    d = bench.DEFAULTS[2]
+    assert bench.workload_name(2, 8, 65536, 64, 2, d["iters"], d["stride"],
+                               d["steps"]) == bench.CONFIG3
+    # another run length keeps the name and says what ran
+    w = bench.workload_name(2, 1, 65536, 64, 2, 1000, 10, 20)
+    assert w.startswith(bench.CONFIG_NAMES[2]) and "20 launches x 1000 iterations" in w
+    # configs[4]'s shape under --config 2 is custom (the config names the 2-source shape)
+    assert bench.workload_name(2, 1, 16384, 128, 3).startswith("custom: ")

@@ -123,14 +123,25 @@ def test_config0_line_beside_one_core():
     assert d["posterior"]["walkers"] == 1 and d["posterior"]["gr_rc_max"] is None
     cb = d["cpu_baseline"]
     assert cb["cores"] == 1 and cb["kind"] == "port" and "1000 iterations" in cb["sample"]
-    assert 0 < cb["reference_over_port"] < 1
-    assert cb["reference_value_derived"] == pytest.approx(cb["value"] * cb["reference_over_port"])
-    assert d["gpu_over_reference"] == pytest.approx(d["value"] / cb["reference_value_derived"])
-    # the reference's loop cost measured here: the astropy-object oracle on one core
     if os.path.exists("/opt/conda/bin/python3.9"):
+        # the reference's loop cost measured here: the astropy-object oracle on one core,
+        # beside the port under the same interpreter (one reference figure,
+        # its ratio like for like); the build container's ratio stays a record only
         rl = cb["reference_like"]
         assert rl["cores"] == 1 and "1000 iterations" in rl["sample"] and rl["value"] > 0
         assert d["gpu_over_reference_like"] == pytest.approx(d["value"] / rl["value"])
+        p39 = rl["port_same_interpreter"]
+        assert p39["cores"] == 1 and "--port" in p39["sample"]
+        assert rl["reference_over_port_same_interpreter"] == pytest.approx(
+            rl["value"] / p39["value"])
+        assert 0 < rl["reference_over_port_same_interpreter"] < 1
+        assert "gpu_over_reference" not in d and "reference_value_derived" not in cb
+        assert 0 < cb["build_container_reference_timing"]["reference_over_port"] < 1
+    else:
+        assert 0 < cb["reference_over_port"] < 1
+        assert cb["reference_value_derived"] == pytest.approx(
+            cb["value"] * cb["reference_over_port"])
+        assert d["gpu_over_reference"] == pytest.approx(d["value"] / cb["reference_value_derived"])
 
 
 def test_per_config_defaults_cover_the_survey_runs():
@@ -250,3 +261,56 @@ def test_csv_emission_reported_outside_the_timed_region():
     c = _line(r)["csv_emission"]
     assert c["files"] == WPG and c["rows_per_file"] == ITERS // STRIDE + 1
     assert c["bytes"] > 0 and c["ms"] > 0 and c["mb_per_s"] > 0
+
+
+def test_per_rank_kernel_times_and_host_overhead_at_world8():
+    """Verdict r04 item 5: a scaling shortfall is attributable from the line.  Rank r's
+    stub launches take 20 + 2r ms, so per_rank_kernel_ms spans 20..34 and
+    host_overhead_frac = 1 - max kernel ms x steps / the max-over-ranks timed region."""
+    r = _run(["--gpus", "8"], {"OLPE_STUB_MS_PER_RANK": "2"})
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    k = d["per_rank_kernel_ms"]
+    assert k["ranks"] == pytest.approx([20.0 + 2 * i for i in range(8)])
+    assert k["min"] == pytest.approx(20.0) and k["max"] == pytest.approx(34.0)
+    elapsed = d["ms_per_step"] * STEPS * 1e-3
+    assert d["host_overhead_frac"] == pytest.approx(1 - 34e-3 * STEPS / elapsed, rel=1e-9)
+    assert 0 <= d["host_overhead_frac"] < 0.5
+    e = d["per_rank_elapsed_s"]
+    assert e["max"] == pytest.approx(elapsed, rel=1e-9) and 0 < e["min"] <= e["max"]
+    # the slowest rank sets the step: at least its 34 ms per launch
+    assert d["ms_per_step"] >= 34.0
+
+
+def test_one_rank_line_carries_the_attribution_fields():
+    r = _run([])
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["per_rank_kernel_ms"]["ranks"] == pytest.approx([20.0])
+    assert 0 <= d["host_overhead_frac"] < 1
+
+
+def test_identical_nodes_repeating_bus_ids_are_not_a_shared_gpu():
+    """two nodes report the same PCI bus id for their GPU 0 -- one rank per
+    node is one process per GPU (accepted); two ranks on one node's GPU are refused."""
+    r = _run(["--gpus", "2"], {"OLPE_STUB_NDEV": "1", "OLPE_STUB_NODES": "2"})
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["config"]["devices"] == [0, 0] and len(d["config"]["pci_bus_ids"]) == 1
+    assert d["config"]["nodes"] == 2
+    r = _run(["--gpus", "3"], {"OLPE_STUB_NDEV": "1", "OLPE_STUB_NODES": "2"})
+    assert r.returncode == 4 and "ranks share a GPU" in r.stderr
+
+
+@pytest.mark.parametrize("args,world,start", [
+    (["--walkers", "2048", "--gpus", "2"], 2, "custom: 2 x 2,048 walkers"),
+    (["--walkers", "65536", "--gpus", "2"], 2, "configs[2]'s shape per GPU, weak-scaled over 2"),
+    (["--walkers", "524288", "--steps", "1"], 1, "custom: 1 x 524,288 walkers"),
+    (["--walkers", "65536", "--gpus", "8", "--steps", "1"], 8, "configs[3]: 524,288 walkers"),
+])
+def test_workload_names_what_ran(args, world, start):
+    """Verdict r04 item 2: the workload names a BASELINE config only at its shape."""
+    r = _run(args, {"OLPE_STUB_MS": "1"})
+    assert r.returncode == 0, r.stderr
+    d = _line(r)
+    assert d["n_gpus"] == world and d["config"]["workload"].startswith(start)

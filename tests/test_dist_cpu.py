@@ -84,6 +84,21 @@ def test_shard_and_seed_helpers():
     assert g.allmax(3.5) == 3.5 and g.broadcast("a") == "a"
 
 
+def test_shared_gpu_verdict_is_per_node():
+    """identical nodes report the same PCI bus ids, so a GPU is a (node, bus
+    id) pair -- two nodes' GPU 0 are two GPUs; two ranks on one node's GPU 0 are not."""
+    a, b = "0000:05:00.0", "0000:06:00.0"
+    assert odist.shared_gpus([("n0", a), ("n1", a)]) == []
+    assert odist.shared_gpus([("n0", a), ("n0", b), ("n1", a), ("n1", b)]) == []
+    assert odist.shared_gpus([("n0", a), ("n1", a), ("n0", a)]) == [("n0", a)]
+    assert odist.node_id()                       # boot id or host name, never empty
+    os.environ["OLPE_NODE_ID"] = "fake"
+    try:
+        assert odist.node_id() == "fake"
+    finally:
+        del os.environ["OLPE_NODE_ID"]
+
+
 def test_bench_comm_watchdog_reports_and_exits():
     """bench.py's watchdog of the end-of-run RCCL exchange: rank 0 prints its JSON line
     with the timeout as comm_error (the measurement survives a hung collective) and the

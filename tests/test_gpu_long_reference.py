@@ -20,18 +20,23 @@ pytestmark = pytest.mark.gpu
 TRAJ = {"exact": 1e-10, "fast": 1e-9}
 
 
-def _run(g, mode):
+def _run(g, mode, reps=1, stats=None):
+    """The fixture's walkers from its start and seeds, every row recorded; ``reps``
+    copies of each walker (walker w runs seed w mod the fixture's count).  ``stats``
+    (a dict) receives the launch's chunks per walker and the hand-off waits."""
     from olpefit_amd.core import Sampler
     nsrc = int(g["nsrc"])
     s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=nsrc)
     s.set_eval_mode(mode)
-    seeds = g["seeds"]
+    seeds = np.tile(g["seeds"], reps)
     s.seed(seeds)
     s.set_state(np.tile(g["p_init"], (len(seeds), 1)))
     L = int(g["traj_len"].min())
     s.enable_trace(True)
     chain = s.run(L, burn_in=0, record_stride=1)
     tr = s.trace(L)
+    if stats is not None:
+        stats.update(units=s.last_units(), waits=int(s.unit_stats()[0]))
     s.close()
     return chain, tr, L
 
@@ -63,3 +68,36 @@ def test_long_chains_match_the_reference(golden, name, mode):
     print(f"{name} {mode}: {L} iterations x {len(g['seeds'])} walkers, max centroid "
           f"difference to the reference {dpx:.3e} px")
     assert dpx <= 1e-3
+
+
+@pytest.mark.parametrize("units", [3, 4])
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+@pytest.mark.parametrize("name", ["c64_long", "c128_3_long", "c32_long", "c64_3_long"])
+def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, units):
+    """Verdict r04 item 3: the chunked work-unit path (configs[1] and
+    configs[4] take P = 3 by default) against the reference's own chains.  With
+    OLPE_UNITS forcing P chunks per walker, each fixture walker's 1,400-5,800
+    iterations run as P consecutive chunks on different waves, handed over through
+    HBM; every row and accept decision must still equal the reference's loop
+    (apf_step2.py:298-338, 3body :324-373).  Each walker runs as 12 / (walkers)
+    copies, so that the launch has the 12 walkers the 128x128 ring sampler needs before
+    it cuts chunks (a lockstep batch must not hold a chunk and its predecessor)."""
+    for k in ("OLPE_NO_QUEUE", "OLPE_RING", "OLPE_WPB"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("OLPE_UNITS", str(units))
+    g = golden(name)
+    nw = len(g["seeds"])
+    reps = -(-12 // nw)
+    st = {}
+    chain, tr, L = _run(g, mode, reps, st)
+    assert st["units"] == units, st
+    assert st["waits"] > 0, st              # chunks really waited on their predecessors
+    ref = g["traj_params"][:, :L]
+    for w in range(nw * reps):
+        np.testing.assert_array_equal(tr[w, :, 5] != 0, g["traj_acc"][w % nw, :L],
+                                      err_msg=f"{name} walker {w}: accept decisions")
+        np.testing.assert_allclose(chain[w], ref[w % nw], rtol=TRAJ[mode],
+                                   err_msg=f"{name} walker {w}")
+    print(f"{name} {mode} P={units}: {nw * reps} walkers x {L} iterations in {units} chunks, "
+          f"{st['waits']} hand-off waits, every row and accept decision equal to the "
+          f"reference's")

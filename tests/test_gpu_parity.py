@@ -338,6 +338,22 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     np.testing.assert_array_equal(s.allgather_chain(0, 1)[0], chain[:1])
     s.gather_limit(0)
     np.testing.assert_array_equal(s.allgather_chain()[0], chain)
+    # the moments all-reduce (verdict r04 item 1): a partials allocation that fails is
+    # OLPE_ENOMEM from the uniformity check, before either all-reduce ...
+    s.moments_fault(1)
+    with pytest.raises(OlpeError) as ei:
+        s.allreduce_moments()
+    assert ei.value.code == -3 and "partials" in str(ei.value)
+    # ... a summary launch that fails after the check still enters both rounds' status
+    # word and returns this rank's error ...
+    s.moments_fault(2)
+    with pytest.raises(OlpeError) as ei:
+        s.allreduce_moments()
+    assert ei.value.code == -2 and "forced" in str(ei.value)
+    # ... and the communicator is still usable: the same summary once cleared
+    s.moments_fault(0)
+    np.testing.assert_array_equal(s.allreduce_moments(), local)
+    np.testing.assert_array_equal(s.allgather_state(), st)
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])

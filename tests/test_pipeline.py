@@ -303,6 +303,16 @@ def test_native_acceptance_files_equal_numpy_str(tmp_path):
     pipeline.write_acceptance_files(a, acc + 1, tries + 2, threads=4)
     assert not list(tmp_path.glob("*.tmp"))
     assert all(open(a[w], "rb").read() != old[w] for w in range(W) if w != 3)
+    # a failed rename (the target is a directory) leaves no '<path>.tmp' either, native
+    # or Python
+    from olpefit_amd._lib import OlpeError
+    d = tmp_path / "dir_target"
+    d.mkdir()
+    with pytest.raises(OlpeError):
+        pipeline.write_acceptance_files([str(d)], acc[:1], tries[:1], threads=1)
+    with pytest.raises(OSError):
+        pipeline.write_acceptance(str(d), acc[0], tries[0])
+    assert not list(tmp_path.glob("*.tmp")) and d.is_dir()
 
 
 def test_native_csv_formatter_equals_repr():
