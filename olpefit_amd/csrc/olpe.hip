@@ -163,7 +163,11 @@ __host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, in
 template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
   return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
 }
-__host__ __device__ constexpr bool ring_wpb(int nt, int wpb) { return nt == 128 && wpb == 12; }
+// (8 waves: the OLPE_DIAG_RING8 diagnostic build only -- the same sweep at 2 waves per
+// SIMD, the bound on the 4-wave layout's gain)
+__host__ __device__ constexpr bool ring_wpb(int nt, int wpb) {
+  return nt == 128 && (wpb == 12 || wpb == 8);
+}
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 // the EXACT samplers' row tables (sweep_exact_rows, [n][G] doubles each): 64x64 2-source
 // dy in the parking area and c*dy^2 in the V-table area; 64x64 3-source c*dy^2 in the
@@ -266,6 +270,8 @@ template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // 4 per CU at 128 VGPRs, +4.5 % over 2 per CU)
 // (hipcc passes the second bound on as the minimum waves per SIMD; the ring sampler,
 // NT = 128 with one 12-wave workgroup per CU, keeps 3 per SIMD with 168 VGPRs)
+// (the diagnostic 8-wave ring keeps the 12-wave one's register budget -- at least 3 waves
+// per SIMD, 168 VGPRs -- so that it runs the same code at 2 waves per SIMD)
 __global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : kGlobalWavesPerEU)
 void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
@@ -941,7 +947,7 @@ size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
   size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring, wpb,
                                     c->eval_mode == OLPE_EVAL_FAST) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
-  if (ring) b += wpb >= 12 ? LdsRing<12>::BYTES : LdsRing<6>::BYTES;
+  if (ring) b += wpb >= 12 ? LdsRing<12>::BYTES : LdsRing<8>::BYTES;
   return b;
 }
 
@@ -1058,8 +1064,12 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
     if constexpr (FAST) {
       // (two 6-wave workgroups per CU with rings of their own -- their control phases
       // apart -- ran at 0.65x: the dispatcher does not pack two of them on a CU)
-      if (c->ring_wpb && c->queue_on && c->d_queue && c->d_uflag)
+      if (c->ring_wpb && c->queue_on && c->d_queue && c->d_uflag) {
+#ifdef OLPE_DIAG_RING8
+        if (c->ring_wpb == 8) return launch_gibbs_t<NSRC, 128, false, 8, FAST>(c, a);
+#endif
         return launch_gibbs_t<NSRC, 128, false, 12, FAST>(c, a);
+      }
     }
     return launch_gibbs_t<NSRC, 128, false, 4, FAST>(c, a);
   }
@@ -1280,7 +1290,12 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   }
   if (const char *e = getenv("OLPE_RING")) {                                // A/B, tests
     const int v = atoi(e);
-    if (v != 0 && v != 12) {
+#ifdef OLPE_DIAG_RING8
+    const bool diag8 = v == 8;      // diagnostic build: the 8-wave ring (2 waves per SIMD)
+#else
+    const bool diag8 = false;
+#endif
+    if (v != 0 && v != 12 && !diag8) {
       olpe_destroy(c);
       return set_err(OLPE_EINVAL, "OLPE_RING=%s: must be 0 (off) or 12 (waves per workgroup)", e);
     }

@@ -1583,7 +1583,7 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 // (Windowed rings without barriers -- four and five slots of 16-row phases -- ran 6 %
 // and 9 % slower; DESIGN_HISTORY.md §7.2, removed in round 4.)
 template <int WAVES> struct LdsRing {
-  static constexpr int ROWS = WAVES >= 12 ? 32 : 16;      // rows per phase
+  static constexpr int ROWS = WAVES >= 8 ? 32 : 16;       // rows per phase
   static constexpr int SLOTS = 2, AHEAD = 1;              // ring slots; DMA lead in phases
   static constexpr int SLOT = ROWS * 64 * 16;
   static constexpr int BYTES = SLOTS * SLOT;
@@ -1607,7 +1607,17 @@ template <int WAVES> struct LdsRing {
     // row rr of phase ph: cutout row ROWS (ph % PPP) + rr, columns 64 (ph / PPP) + lane
     const int row = (ph % PPP) * ROWS + rr;
     const double2 *src = DW + row * 128 + (ph / PPP) * 64;
-    const unsigned dst = lds + (unsigned)(sl * SLOT + rr * 1024);
+    unsigned dst = lds + (unsigned)(sl * SLOT + rr * 1024);
+    if constexpr (WAVES != 12) {
+      // (the diagnostic 8-wave ring: the compiler loses the uniformity of the address
+      // there; the 12-wave code is left exactly as it was)
+      dst = (unsigned)__builtin_amdgcn_readfirstlane((int)dst);
+      src = reinterpret_cast<const double2 *>(
+          (((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane(
+               (int)((unsigned long long)src >> 32)))
+           << 32) |
+          (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned long long)src));
+    }
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"

@@ -81,23 +81,31 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
     HBM; every row and accept decision must still equal the reference's loop
     (apf_step2.py:298-338, 3body :324-373).  Each walker runs as 12 / (walkers)
     copies, so that the launch has the 12 walkers the 128x128 ring sampler needs before
-    it cuts chunks (a lockstep batch must not hold a chunk and its predecessor)."""
+    it cuts chunks (a lockstep batch must not hold a chunk and its predecessor).  The
+    ring sampler hands out batches of 12 units to whole workgroups, so 12 walkers are one
+    workgroup running its chunks one after the other (hand-offs through HBM without a
+    wait); it runs 768 walkers instead -- 64 workgroups, whose chunk-1 batches land on
+    other workgroups than their predecessors and wait for them."""
     for k in ("OLPE_NO_QUEUE", "OLPE_RING", "OLPE_WPB"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("OLPE_UNITS", str(units))
     g = golden(name)
     nw = len(g["seeds"])
-    reps = -(-12 // nw)
+    ring = name.startswith("c128") and mode == "fast"
+    reps = 768 // nw if ring else -(-12 // nw)
     st = {}
     chain, tr, L = _run(g, mode, reps, st)
     assert st["units"] == units, st
     assert st["waits"] > 0, st              # chunks really waited on their predecessors
     ref = g["traj_params"][:, :L]
-    for w in range(nw * reps):
-        np.testing.assert_array_equal(tr[w, :, 5] != 0, g["traj_acc"][w % nw, :L],
-                                      err_msg=f"{name} walker {w}: accept decisions")
-        np.testing.assert_allclose(chain[w], ref[w % nw], rtol=TRAJ[mode],
-                                   err_msg=f"{name} walker {w}")
+    ps = ref.shape[-1]
+    # walker w runs fixture walker w mod nw: [reps, nw, ...] against the fixture
+    acc = tr[:, :, 5].reshape(reps, nw, L) != 0
+    bad = np.argwhere(acc != g["traj_acc"][None, :, :L])
+    assert bad.size == 0, f"{name}: accept decisions differ at (copy, walker, iteration) {bad[:5]}"
+    np.testing.assert_allclose(chain.reshape(reps, nw, L, ps),
+                               np.broadcast_to(ref, (reps, nw, L, ps)), rtol=TRAJ[mode],
+                               err_msg=name)
     print(f"{name} {mode} P={units}: {nw * reps} walkers x {L} iterations in {units} chunks, "
           f"{st['waits']} hand-off waits, every row and accept decision equal to the "
           f"reference's")

@@ -35,7 +35,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 PEAK = 78.6e12 / 2
 GIBBS = "olpe_gibbs_kernel"
-KEEP = (GIBBS, "fold_kernel", "summary_stage")
+KEEP = (GIBBS, "fold_rows_kernel", "fold_cols_kernel", "summary_stage")
 FP64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
         "SQ_INSTS_VALU_TRANS_F64")
 
