@@ -160,18 +160,13 @@ __host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, in
 // the ring sampler's per-wave slice: the WaveSlice fields up to the parking area, the
 // draw tables there (its sweeps park nothing) and the two FAST3 shape-table slots (no
 // V-table fallback)
-// (the 16-wave ring: ONE shape-table slot per wave, rebuilt in place with stale-set
-// tracking as the 64x64 16-wave sampler's, so that 16 slices fit beside the ring)
-template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n, int wpb = 12) {
-  return WaveSlice<NP>::OPE + kDrawTabBytes + (wpb >= 16 ? 1 : 2) * n * 16;
+template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
+  return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
 }
-// the ring sampler's LDS header: the exp table, the batch word and one iteration count
-// per wave (s_prog[2 + wave]): 16 waves need 72 bytes after the table
-__host__ __device__ constexpr int ring_hdr(int wpb) { return wpb > 14 ? kEtabBytes + 128 : kSampHdr; }
 // (8 waves: the OLPE_DIAG_RING8 diagnostic build only -- the same sweep at 2 waves per
-// SIMD; 16 waves, 4 per SIMD: OLPE_RING=16, the two-row update in 128 VGPRs, round 5)
+// SIMD, the bound on the 4-wave layout's gain)
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) {
-  return nt == 128 && (wpb == 12 || wpb == 8 || wpb == 16);
+  return nt == 128 && (wpb == 12 || wpb == 8);
 }
 static_assert((WaveSlice<16>::U32 * 4) % 8 == 0 && (WaveSlice<19>::U32 * 4) % 8 == 0, "align");
 // the EXACT samplers' row tables (sweep_exact_rows, [n][G] doubles each): 64x64 2-source
@@ -277,7 +272,7 @@ template <int NSRC, int NT, bool LDS_IMG, int WPB, bool FAST>
 // NT = 128 with one 12-wave workgroup per CU, keeps 3 per SIMD with 168 VGPRs)
 // (the diagnostic 8-wave ring keeps the 12-wave one's register budget -- at least 3 waves
 // per SIMD, 168 VGPRs -- so that it runs the same code at 2 waves per SIMD)
-__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB >= 12)) ? 1 : kGlobalWavesPerEU)
+__global__ __launch_bounds__(WPB * 64, (LDS_IMG || (NT == 128 && WPB == 12)) ? 1 : kGlobalWavesPerEU)
 void olpe_gibbs_kernel(GibbsArgs A) {
   using L = Layout<NSRC>;
   using WS = WaveSlice<L::NP>;
@@ -296,10 +291,9 @@ void olpe_gibbs_kernel(GibbsArgs A) {
   // ---- LDS carve: exp table, [DE] (if staged), then one {WaveSlice, V table} per wave
   double *etab = reinterpret_cast<double *>(smem);
   unsigned *s_prog = reinterpret_cast<unsigned *>(smem + kEtabBytes);  // progress balancing
-  constexpr int HDR = RING ? ring_hdr(WPB) : kSampHdr;
-  double2 *sDE = reinterpret_cast<double2 *>(smem + HDR);
+  double2 *sDE = reinterpret_cast<double2 *>(smem + kSampHdr);
   constexpr int TABX = drawtab_extra(NT, FAST);
-  const int wstride = RING ? ring_wave_bytes<NP>(n, WPB)
+  const int wstride = RING ? ring_wave_bytes<NP>(n)
                            : WS::BYTES + TABX + sampler_vtab_bytes(n, NSRC, NT, WPB, FAST);
   unsigned char *wb = reinterpret_cast<unsigned char *>(sDE + (LDS_IMG ? npix : 0)) +
                       (RING ? Ring::BYTES : 0) + (size_t)wave * wstride;
@@ -320,7 +314,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
   __syncthreads();
   const double2 *DE = LDS_IMG ? sDE : A.DE;
   [[maybe_unused]] Ring ring;
-  if constexpr (RING) ring.prologue(smem + HDR, A.DE, wave, lane);
+  if constexpr (RING) ring.prologue(smem + kSampHdr, A.DE, wave, lane);
   unsigned my_steps = 0;   // iterations this wave has started in this launch
   // start offset: the waves of a SIMD (wave, wave + 4, wave + 8) start a fraction of a
   // step apart so that their latency-bound control phases do not coincide
@@ -470,7 +464,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     double *chain_w = K()->chain + (size_t)w * nrows * PS;
 
     HCache hcache;
-    hcache.single = single_h(NSRC, NT, WPB, FAST) || (RING && WPB >= 16);
+    hcache.single = single_h(NSRC, NT, WPB, FAST);
     GuardCache gcache;
     ColCache<2 * NSRC> ccache;     // FAST3 column terms of the current state
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
@@ -904,7 +898,7 @@ template <class T> int dev_alloc(T **p, size_t count) {
 // pixels, otherwise NT = 0 / 128 (no extra draw-table bytes)
 size_t wave_lds(int n, int np, bool lds_img, bool ring = false, int wpb = 12,
                 bool fast = false) {
-  if (ring) return (size_t)(np == 16 ? ring_wave_bytes<16>(n, wpb) : ring_wave_bytes<19>(n, wpb));
+  if (ring) return (size_t)(np == 16 ? ring_wave_bytes<16>(n) : ring_wave_bytes<19>(n));
   const int nt = lds_img && (n == 32 || n == 64) ? n : 0;
   return (size_t)(np == 16 ? WaveSlice<16>::BYTES : WaveSlice<19>::BYTES) +
          drawtab_extra(nt, fast) + sampler_vtab_bytes(n, np == 16 ? 2 : 3, nt, wpb, fast);
@@ -951,8 +945,7 @@ int choose_units(long long W, long long slots, long long n_iters, int override_p
 
 size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
   size_t b = (size_t)wpb * wave_lds(c->n, c->np, c->lds_img, ring, wpb,
-                                    c->eval_mode == OLPE_EVAL_FAST) +
-             (ring ? ring_hdr(wpb) : kSampHdr);
+                                    c->eval_mode == OLPE_EVAL_FAST) + kSampHdr;
   if (c->lds_img) b += (size_t)c->n * c->n * sizeof(double2);
   if (ring) b += wpb >= 12 ? LdsRing<12>::BYTES : LdsRing<8>::BYTES;
   return b;
@@ -1075,7 +1068,6 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
 #ifdef OLPE_DIAG_RING8
         if (c->ring_wpb == 8) return launch_gibbs_t<NSRC, 128, false, 8, FAST>(c, a);
 #endif
-        if (c->ring_wpb == 16) return launch_gibbs_t<NSRC, 128, false, 16, FAST>(c, a);
         return launch_gibbs_t<NSRC, 128, false, 12, FAST>(c, a);
       }
     }
@@ -1303,9 +1295,9 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
 #else
     const bool diag8 = false;
 #endif
-    if (v != 0 && v != 12 && v != 16 && !diag8) {
+    if (v != 0 && v != 12 && !diag8) {
       olpe_destroy(c);
-      return set_err(OLPE_EINVAL, "OLPE_RING=%s: must be 0 (off), 12 or 16 (waves per workgroup)", e);
+      return set_err(OLPE_EINVAL, "OLPE_RING=%s: must be 0 (off) or 12 (waves per workgroup)", e);
     }
     c->ring_wpb = v;
   }

@@ -1674,17 +1674,13 @@ template <int WAVES> struct LdsRing {
 // FAST3 sweep of a 128x128 cutout from the ring (sweep_fast3's NT > 64 form otherwise:
 // column terms from the step's col_coef coefficients, four-row update, shape-table
 // prefetch).  Two passes x 32 four-row blocks; a phase (four blocks) opens with
-// begin_phase just before its first block is prefetched.  The 16-wave ring (4 waves per
-// SIMD, 128 VGPRs) updates two rows at a time instead: 16 blocks of two rows per phase,
-// 3m - 1 operations per two rows and shape set (m Gaussians) against 5m - 1 per four --
-// the powers rho^r of six Gaussians are 24 VGPRs instead of 48.
+// begin_phase just before its first block is prefetched.
 template <int NSRC, int WAVES>
 __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, const double *htab,
                                                    int lane, ExpTab ex, const double *colc,
                                                    LdsRing<WAVES> &ring) {
   constexpr int G = 2 * NSRC;
-  constexpr int RU = WAVES >= 16 ? 2 : 4;           // rows per update
-  constexpr int BLK = RU, NB = 128 / BLK;           // 32 (64) blocks per pass
+  constexpr int BLK = 4, RU = 4, NB = 128 / BLK;    // 32 blocks per pass
   constexpr int BPP = LdsRing<WAVES>::ROWS / BLK;   // blocks per phase
   const double bg = m.bg;
   const double2 *hr = reinterpret_cast<const double2 *>(htab);
@@ -1704,17 +1700,13 @@ __device__ __forceinline__ double sweep_fast3_ring(const ModelDesc<NSRC> &m, con
       rho0[g] = t.R;
       __builtin_amdgcn_sched_barrier(0);
     }
-    double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^RU
+    double rp[RU][G];                  // rp[r] = rho^r, rp[0] = rho^4
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       rp[1][g] = rho[g];
-      if constexpr (RU == 4) {
-        rp[2][g] = rho[g] * rho[g];
-        rp[3][g] = rp[2][g] * rho[g];
-        rp[0][g] = rp[2][g] * rp[2][g];
-      } else {
-        rp[0][g] = rho[g] * rho[g];
-      }
+      rp[2][g] = rho[g] * rho[g];
+      rp[3][g] = rp[2][g] * rho[g];
+      rp[0][g] = rp[2][g] * rp[2][g];
     }
     auto row4 = [&](const double2 *h, const double2 *dw) {
       double sw[RU], sn[RU];

@@ -110,29 +110,3 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
           f"{st['waits']} hand-off waits, every row and accept decision equal to the "
           f"reference's")
 
-
-@pytest.mark.parametrize("units", [1, 3])
-def test_long_chains_sixteen_wave_ring(golden, monkeypatch, units):
-    """The 16-wave ring sampler (OLPE_RING=16, round 5) against the reference's own
-    128x128 3-source loop (c128_3_long): every row within the FAST trajectory tolerance
-    and every accept decision equal, 768 copies of the fixture's walkers (64 workgroups),
-    whole walkers and P = 3 chunks."""
-    for k in ("OLPE_NO_QUEUE", "OLPE_WPB"):
-        monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("OLPE_RING", "16")
-    monkeypatch.setenv("OLPE_UNITS", str(units))
-    g = golden("c128_3_long")
-    nw = len(g["seeds"])
-    reps = 768 // nw
-    st = {}
-    chain, tr, L = _run(g, "fast", reps, st)
-    assert st["units"] == units, st
-    if units > 1:
-        assert st["waits"] > 0, st
-    ref = g["traj_params"][:, :L]
-    ps = ref.shape[-1]
-    acc = tr[:, :, 5].reshape(reps, nw, L) != 0
-    bad = np.argwhere(acc != g["traj_acc"][None, :, :L])
-    assert bad.size == 0, f"accept decisions differ at (copy, walker, iteration) {bad[:5]}"
-    np.testing.assert_allclose(chain.reshape(reps, nw, L, ps),
-                               np.broadcast_to(ref, (reps, nw, L, ps)), rtol=TRAJ["fast"])

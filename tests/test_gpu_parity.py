@@ -757,53 +757,6 @@ def test_ring_sampler_equals_l2_sampler(lib_loaded, monkeypatch, ring, units):
     np.testing.assert_array_equal(da, db)
 
 
-@pytest.mark.parametrize("units", [0, 1, 3])
-def test_sixteen_wave_ring_sampler(lib_loaded, monkeypatch, units):
-    """The 16-wave ring sampler (OLPE_RING=16, round 5: 4 waves per SIMD in 128 VGPRs,
-    one shape-table slot per wave rebuilt in place, the two-row update) against the
-    L2-resident sampler: its rows sum the geometric terms two rows at a time instead of
-    four, so values agree to rounding (FAST trajectory tolerance, rtol 1e-9) and every
-    draw, accept decision, counter, RNG state and done_at is identical -- the same
-    1,001 walkers, odd launch bounds and accept_min stop as the 12-wave test."""
-    from olpefit_amd import synth
-    from olpefit_amd.core import Sampler
-    from olpefit_amd.pipeline import initial_parameters
-    n, nsrc, W = 128, 3, 1001
-    img, _ = synth.make_image(n, nsrc, 0)
-    p0 = initial_parameters(img, synth.guess_values(n, nsrc), nsrc)
-    out = []
-    for rg, no_queue, u in (("0", "1", 0), ("16", "0", units)):
-        monkeypatch.setenv("OLPE_RING", rg)
-        monkeypatch.setenv("OLPE_NO_QUEUE", no_queue)
-        monkeypatch.setenv("OLPE_UNITS", str(u))
-        s = Sampler(img, 1.0, 1, 1, 2, nsrc=nsrc)
-        p0[-1] = s.chi_squared(p0)
-        s.seed(3000 + np.arange(W))
-        s.set_state(np.tile(p0, (W, 1)))
-        s.enable_trace(True)
-        chains, traces = [], []
-        for it, burn, stride in ((31, 7, 5), (45, 0, 4), (17, 60, 3)):
-            chains.append(s.run(it, burn_in=burn, record_stride=stride, accept_min=4))
-            traces.append(s.trace(it))
-        out.append((chains, traces, s.get_state(), s.rng_state(), s.done_at(),
-                    s.last_units()))
-        s.close()
-    (ca, ta, sa, ra, da, _), (cb, tb, sb, rb, db, ub) = out
-    if units:
-        assert ub == units
-    for x, y in zip(ca, cb):
-        np.testing.assert_allclose(y, x, rtol=1e-9)
-    for x, y in zip(ta, tb):
-        for f in (0, 3, 5):                  # index, dice, accept: identical
-            np.testing.assert_array_equal(y[..., f], x[..., f])
-        np.testing.assert_allclose(y[..., 1:3], x[..., 1:3], rtol=1e-9)
-    np.testing.assert_allclose(sb[0], sa[0], rtol=1e-9)
-    for x, y in zip(sa[1:] + ra, sb[1:] + rb):
-        np.testing.assert_array_equal(x, y)
-    np.testing.assert_array_equal(da, db)
-    assert np.any(sa[2] > 0)
-
-
 def test_ring_sampler_few_walkers_forced_units(lib_loaded, monkeypatch):
     """A lockstep batch must not hold a chunk and its predecessor (the chunk would wait
     for a wave that waits at the batch's barrier): with fewer walkers than a batch the

@@ -16,7 +16,12 @@ u(3) / u(2) fixes p, and u(4) / u(3) is then the most a fourth wave can add at t
 instructions per walker-step -- before the extra instructions a 128-VGPR layout costs
 (the two-row update: 12 instead of 11 FP64 per pixel with three sources).  Since waves
 do not stall independently (they share the lockstep barriers), the model overstates
-what a fourth wave adds, so it is an upper bound.
+what a fourth wave adds, so it is an upper bound.  (Measured, round 5: the issue
+fraction rose 1.68x from 2 to 3 waves -- more than the 1.5x of the waves themselves --
+so the model's fit degenerates to p -> 0, u(k) proportional to k, and the bound is the
+linear one, 4/3: not below 3 %.  The 16-wave ring was then built and measured,
+profiles/r05/ring16/summary.json: issue 0.72 -> 0.82 at the held clock, eaten by 12.8 %
+more VALU per walker-step; level, -0.6 %.)
 """
 import csv
 import json
@@ -74,10 +79,11 @@ def one(d, log_dir, rg, rep):
 
 def main():
     src, dst = sys.argv[1:3]
+    waves = [int(x) for x in sys.argv[3:]] or [12, 8]
     os.makedirs(dst, exist_ok=True)
     res = []
     for rep in (1, 2):
-        for rg in (12, 8):
+        for rg in waves:
             d = os.path.join(src, f"w{rg}_{rep}")
             if not os.path.isdir(d):
                 continue
@@ -100,6 +106,18 @@ def main():
 
     def mean(rg, k):
         return statistics.fmean(r[k] for r in res if r["waves_per_workgroup"] == rg)
+
+    if 8 not in waves:
+        # another pair (the 16-wave ring against the 12-wave one): the runs side by side
+        out = {"runs": res}
+        for rg in waves:
+            out[f"w{rg}"] = {k: mean(rg, k) for k in ("kernel_walker_steps_per_s",
+                             "valu_per_walker_step", "fp64_lane_ops_per_walker_step",
+                             "clock_ghz", "valu_issue_frac_spec", "valu_issue_frac_held_clock")}
+        with open(os.path.join(dst, "summary.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps({k: v for k, v in out.items() if k != "runs"}, indent=1))
+        return
 
     u2 = mean(8, "valu_issue_frac_held_clock")
     u3 = mean(12, "valu_issue_frac_held_clock")
