@@ -24,7 +24,8 @@ def test_metric_is_baselines():
 
 @pytest.mark.parametrize("where,name,cfg", [
     ("r03", "bench", 2), ("r03", "bench_c1", 1), ("r03", "bench_c4", 4),
-    ("r04/final", "bench", 2), ("r04/final", "bench_c1", 1), ("r04/final", "bench_c4", 4)])
+    ("r04/final", "bench", 2), ("r04/final", "bench_c1", 1), ("r04/final", "bench_c4", 4),
+    ("r05/final", "bench", 2), ("r05/final", "bench_c1", 1), ("r05/final", "bench_c4", 4)])
 def test_committed_bench_lines(where, name, cfg):
     d = _last_json(os.path.join(REPO, "profiles", where, f"{name}.log"))
     assert d["metric"] == bench.METRIC and d["unit"] == "walker-steps/s"
@@ -55,16 +56,36 @@ def test_committed_bench_lines(where, name, cfg):
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "walker-steps/s" and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["sample"]
-    if where.startswith("r04"):
-        # round 4: SURVEY 8(d)'s shape per config, the reference/port ratio, the held clock
+    if where.startswith(("r04", "r05")):
+        # round 4: SURVEY 8(d)'s shape per config, the held clock
         dflt = bench.DEFAULTS[cfg]
         assert c["iters_per_step"] == dflt["iters"] and c["chain_stride"] == dflt["stride"]
         assert d["steps"] * c["iters_per_step"] == {1: 10000, 2: 2000, 4: 500}[cfg]
         assert p["tag"] == "r04" and 0 < p["frac_of_held_clock_peak"] < 1
+        assert c["devices"] == [0] and c["launcher"] == "none (1 rank)"
+    if where.startswith("r04"):
+        # the reference/port ratio of the build container turned into a derived rate
         assert 0 < cb["reference_over_port"] < 1
         assert d["gpu_over_reference"] == pytest.approx(
             d["value"] / (cb["value"] * cb["reference_over_port"]), rel=1e-9)
-        assert c["devices"] == [0] and c["launcher"] == "none (1 rank)"
+    if where.startswith("r05"):
+        # round 5: one reference figure (measured on the box), the port also timed under
+        # that figure's interpreter, and the line's own attribution of the step
+        assert "gpu_over_reference" not in d and "reference_value_derived" not in cb
+        rl = cb["reference_like"]
+        assert 0 < rl["reference_over_port_same_interpreter"] < 1
+        assert rl["reference_over_port_same_interpreter"] == pytest.approx(
+            rl["value"] / rl["port_same_interpreter"]["value"], rel=1e-9)
+        assert d["per_rank_kernel_ms"]["ranks"] == [r["kernel_ms"]]
+        assert d["host_overhead_frac"] == pytest.approx(
+            1 - r["kernel_ms"] * 1e-3 * d["steps"] / (d["ms_per_step"] * d["steps"] * 1e-3),
+            rel=1e-6)
+        assert 0 <= d["host_overhead_frac"] < 0.03
+        # the profiling session of this round reproduces the line's frac (verdict r04
+        # item 6): profiles/r05/roofline.json
+        with open(os.path.join(REPO, "profiles", "r05", "roofline.json")) as f:
+            sess = json.load(f)[{1: "c1_fast", 2: "fast", 4: "c4_fast"}[cfg]]
+        assert abs(r["frac"] / sess["frac"] - 1) < 0.03
 
 
 def test_committed_config0_line():
