@@ -271,6 +271,57 @@ def make_long_case(name, n, nsrc, n_walkers, accept_min, burn_in):
     print(name, "iterations per walker:", list(lens))
 
 
+def _posterior_walker(args):
+    spec_name, n, nsrc, seed, accept_min = args
+    spec = TWO if spec_name == "two" else THREE
+    np.seterr(all="ignore")
+    image, _ = synth.make_image(n, nsrc, seed=0)
+    image = image.astype(">f4")
+    header = dict((k.lower(), v) for k, v in synth.HEADER.items())
+    guess = synth.guess_values(n, nsrc)
+    with tempfile.TemporaryDirectory() as td:
+        tr, p0, ns = run_reference_loop(spec, image, header, guess, int(seed), accept_min,
+                                        10 ** 9, td, 0)
+    rows = np.array([t[5] for t in tr])
+    accs = np.array([t[4] for t in tr])
+    draws = np.array([t[0] for t in tr], np.uint8)
+    return (rows, accs, p0, np.asarray(ns["total_tries"], np.float64),
+            np.asarray(ns["total_accept"], np.float64), draws)
+
+
+def make_posterior_case(name, n, nsrc, n_walkers, accept_min, every=50):
+    """Round 5: ~20,000-iteration chains of the reference's own loop (the verdict's
+    'posterior runs are oracle-only'), stored compactly: every ``every``-th row, every
+    accept decision (bit-packed), each walker's whole-chain mean and sum of squared
+    deviations per column (what step 3's statistics need, apf_step3.py:258-278), the
+    tries / accepts counters and the final state.  Walkers run in parallel processes."""
+    import multiprocessing as mp
+    seeds = np.arange(1000, 1000 + n_walkers)
+    with mp.get_context("fork").Pool(min(n_walkers, os.cpu_count() or 1)) as pool:
+        res = pool.map(_posterior_walker, [("two" if nsrc == 2 else "three", n, nsrc, int(s),
+                                            accept_min) for s in seeds])
+    lens = np.array([len(r[0]) for r in res])
+    L = int(lens.min())                   # every walker's first L iterations
+    P = res[0][2].size
+    sub = np.arange(every - 1, L, every)  # rows after iterations every, 2 every, ...
+    rows_sub = np.array([r[0][sub] for r in res])
+    acc_bits = np.array([np.packbits(r[1][:L]) for r in res])
+    mean = np.array([r[0][:L].mean(axis=0) for r in res])
+    m2 = np.array([((r[0][:L] - r[0][:L].mean(axis=0)) ** 2).sum(axis=0) for r in res])
+    # (the draws -- the parameter index of every iteration -- and the accept bits give
+    # the tries / accepts after L iterations; the reference's total_tries / total_accept
+    # at its own stop are kept as well)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), image=np.asarray(
+        synth.make_image(n, nsrc, seed=0)[0].astype(">f4"), np.float32),
+        guess=np.array(synth.guess_values(n, nsrc)), p_init=res[0][2], seeds=seeds,
+        traj_len=lens, L=np.int64(L), every=np.int64(every), rows_sub=rows_sub,
+        acc_bits=acc_bits, draws=np.array([r[5][:L] for r in res]), mean=mean, m2=m2,
+        final=np.array([r[0][L - 1] for r in res]),
+        stop_tries=np.array([r[3] for r in res]), stop_accepts=np.array([r[4] for r in res]),
+        accept_min=np.int64(accept_min), nsrc=np.int64(nsrc))
+    print(name, "iterations per walker:", list(lens), "kept", L, "P", P, flush=True)
+
+
 def make_rng():
     seeds = [0, 1, 5489, 12345, 2 ** 32 - 1] + list(range(1000, 1008))
     raw, gauss, unif, ri16, ri19 = [], [], [], [], []
@@ -325,6 +376,12 @@ if __name__ == "__main__":
         # 64x64 cutout past 2,000
         make_long_case("c32_long", 32, 2, n_walkers=2, accept_min=75, burn_in=0)
         make_long_case("c64_3_long", 64, 3, n_walkers=2, accept_min=115, burn_in=0)
+        sys.exit(0)
+    if sys.argv[1:] == ["posterior"]:
+        # round 5: ~20,000 iterations per walker from the reference's own loop, 8 walkers
+        # at 64x64 (2 sources) and 4 at 128x128 (3 sources)
+        make_posterior_case("c64_post", 64, 2, n_walkers=8, accept_min=1200)
+        make_posterior_case("c128_3_post", 128, 3, n_walkers=4, accept_min=1000)
         sys.exit(0)
     if sys.argv[1:] == ["nonfinite3"]:
         # round 4: the 3-source twins with non-finite data pixels (3body

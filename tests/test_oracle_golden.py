@@ -159,3 +159,22 @@ def test_astropy_oracle_is_the_reference(name, walker, iters):
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["rows"] == iters and d["bit_equal"] is True
+
+
+def test_oracle_posterior_run_matches_reference(golden):
+    """Round 5's posterior fixture (make_golden.py ``posterior``: the reference's own
+    loop, ~20,000 iterations per walker, stored as every 50th row, every draw and accept
+    decision, and each walker's whole-chain mean / M2): walker 0 of the 64x64 case from
+    the oracle -- every draw and decision, the stored rows and the walker's moments."""
+    g = golden("c64_post")
+    nsrc = int(g["nsrc"])
+    L, every = int(g["L"]), int(g["every"])
+    dm, err, _, _ = ora.noise_model(g["image"], 1.0, 1, 1, 2)
+    w = ora.Walker(dm, err, g["p_init"], int(g["seeds"][0]), nsrc)
+    chain, tr = w.run(L, trace=True)
+    assert np.array_equal(np.array([t[0] for t in tr], np.uint8), g["draws"][0])
+    assert np.array_equal(np.packbits(np.array([t[4] for t in tr], bool)), g["acc_bits"][0])
+    np.testing.assert_allclose(chain[every - 1::every], g["rows_sub"][0], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(chain.mean(axis=0), g["mean"][0], rtol=1e-13)
+    np.testing.assert_allclose(((chain - chain.mean(axis=0)) ** 2).sum(axis=0), g["m2"][0],
+                               rtol=1e-8)
