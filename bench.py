@@ -931,19 +931,18 @@ def main():
         out["cpu_baseline"] = cb
         out["gpu_over_cpu"] = value / cb["value"]
         if not args.no_reference_like:
-            rl = (reference_like_baseline(n, nsrc, 1000, procs=1) if args.config == 0
-                  else reference_like_baseline(n, nsrc, args.cpu_steps_ref or max(
-                      1600, 24000 * 64 * 64 // (n * n))))
+            # configs[0]: one walker on one core, the reference's 1,000 iterations
+            ref_steps, ref_procs = ((1000, 1) if args.config == 0 else
+                                    (args.cpu_steps_ref or max(1600, 24000 * 64 * 64 // (n * n)),
+                                     None))
+            rl = reference_like_baseline(n, nsrc, ref_steps, procs=ref_procs)
             if rl:
                 # the reference's loop cost measured on these cores (the astropy-object
                 # oracle), beside the NumPy port above; and the port under the same
                 # python3.9, so that their ratio is like for like
                 cb["reference_like"] = rl
                 out["gpu_over_reference_like"] = value / rl["value"]
-                p39 = (reference_like_baseline(n, nsrc, 1000, procs=1, port=True)
-                       if args.config == 0 else reference_like_baseline(
-                           n, nsrc, args.cpu_steps_ref or max(1600, 24000 * 64 * 64 // (n * n)),
-                           port=True))
+                p39 = reference_like_baseline(n, nsrc, ref_steps, procs=ref_procs, port=True)
                 if p39:
                     rl["port_same_interpreter"] = p39
                     rl["reference_over_port_same_interpreter"] = rl["value"] / p39["value"]
