@@ -1536,8 +1536,16 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         const int hb = more ? b0 + BLK : b0;
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
+#if defined(OLPE_DIAG_DWCONST)
+          nxt[k] = NT > 64 ? img(hb + k) : (DW + jj)[k * rstep];   // (diagnostic: meaningless)
+#else
           nxt[k] = NT > 64 ? img(hb + k) : pn[k * rstep];
+#endif
+#if defined(OLPE_DIAG_HCONST)
+          hn[k] = hr[k];                                   // (diagnostic: results meaningless)
+#else
           hn[k] = hr[hb + k];
+#endif
         }
 #pragma unroll
         for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
