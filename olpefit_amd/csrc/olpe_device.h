@@ -1543,6 +1543,18 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
 #endif
 #if defined(OLPE_DIAG_HCONST)
           hn[k] = hr[k];                                   // (diagnostic: results meaningless)
+#elif defined(OLPE_DIAG_HSMEM)
+          {
+            // (diagnostic, results meaningless: the rows by scalar loads from constant
+            // global memory -- the kernel's cutout, GibbsArgs::DE at kernarg offset 0, one
+            // table shared by every wave -- the bound for scalar-loaded rows)
+            typedef __attribute__((address_space(4))) const double c_f64;
+            const __attribute__((address_space(4))) unsigned long long *ka =
+                (const __attribute__((address_space(4))) unsigned long long *)
+                    __builtin_amdgcn_kernarg_segment_ptr();
+            const c_f64 *hq = (const c_f64 *)ka[0];
+            hn[k] = make_double2(hq[2 * (hb + k)], hq[2 * (hb + k) + 1]);
+          }
 #else
           hn[k] = hr[hb + k];
 #endif
