@@ -1628,7 +1628,12 @@ template <int WAVES> struct LdsRing {
     const int row = (ph % PPP) * ROWS + rr;
     const double2 *src = DW + row * 128 + (ph / PPP) * 64;
     unsigned dst = lds + (unsigned)(sl * SLOT + rr * 1024);
-    if constexpr (WAVES != 12) {
+#ifdef OLPE_DIAG_TIMING
+    constexpr bool kFirstLane = true;         // (the timing build loses it too)
+#else
+    constexpr bool kFirstLane = WAVES != 12;
+#endif
+    if constexpr (kFirstLane) {
       // (the diagnostic 8-wave ring: the compiler loses the uniformity of the address
       // there; the 12-wave code is left exactly as it was)
       dst = (unsigned)__builtin_amdgcn_readfirstlane((int)dst);
