@@ -48,6 +48,11 @@ template <int NSRC> __device__ __forceinline__ double width_of(int r) {
 }
 
 struct GibbsArgs {
+#ifdef OLPE_DIAG_HSMEM_PW
+  // (diagnostic build only, first so that it sits at kernarg offset 0 where the
+  // OLPE_DIAG_HSMEM hook reads its table base: 64 KiB of finite doubles per wave slot)
+  const double *diag_h;
+#endif
   const double2 *DE;   // [n*n] {data, 1/err} (EXACT) or {data/err, 1/err} (FAST); {0,0} masked
   int n;
   int bkgd_mode;
@@ -951,6 +956,13 @@ size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
   return b;
 }
 
+#ifdef OLPE_DIAG_HSMEM_PW
+__global__ void diag_fill_kernel(double2 *out, size_t n, const double2 *src, size_t npix) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[i % npix];
+}
+#endif
+
 template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   constexpr bool RING = !LDS && FAST && ring_wpb(NT, WPB);    // (olpe_gibbs_kernel)
@@ -1015,6 +1027,26 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
                        : (unsigned long long)std::min(std::max(ticks, 3e9), 1e15);
     c->wait_limit_s = (double)q.wait_ticks * 1e-8;
   }
+#ifdef OLPE_DIAG_HSMEM_PW
+  {
+    // (diagnostic build only: a 64 KiB region per wave slot, the cutout repeated)
+    static double *diag_buf = nullptr;
+    static size_t diag_cap = 0;
+    const size_t need = (size_t)blocks * WPB * 65536;
+    if (need > diag_cap) {
+      if (diag_buf) (void)hipFree(diag_buf);
+      diag_buf = nullptr;
+      diag_cap = 0;
+      HIPCHK(hipMalloc((void **)&diag_buf, need));
+      diag_cap = need;
+      const size_t n2 = need / 16, npix = (size_t)a.n * a.n;
+      hipLaunchKernelGGL(diag_fill_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0,
+                         c->stream, reinterpret_cast<double2 *>(diag_buf), n2, a.DE, npix);
+      HIPCHK(hipGetLastError());
+    }
+    q.diag_h = diag_buf;
+  }
+#endif
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
   // the launch takes W * units + (its waves) values off the counter (the ring sampler:

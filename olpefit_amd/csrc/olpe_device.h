@@ -1271,6 +1271,9 @@ template <int G> struct ColCache {
 #ifdef OLPE_DIAG_TIMING
   unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
 #endif
+#ifdef OLPE_DIAG_HSMEM_ROT
+  int dver = 0;                          // (diagnostic: sweeps so far, the table version)
+#endif
 };
 
 // The proposal's column terms of the Gaussians it moves (gauss_mask: 0, 2 or NSRC of
@@ -1329,6 +1332,9 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
   const double yr = (double)cw.grp;
   const double bg = m.bg;
   double acc = 0.0;
+#ifdef OLPE_DIAG_HSMEM_ROT
+  if constexpr (CC) ++cc->dver;
+#endif
   [[maybe_unused]] double rho0[G];     // NT = 128: pass 0's rho (col_term64_pass1)
   for (int c0 = 0; c0 < n; c0 += 64) {
     const int j = c0 + cw.jl;
@@ -1553,7 +1559,24 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
                 (const __attribute__((address_space(4))) unsigned long long *)
                     __builtin_amdgcn_kernarg_segment_ptr();
             const c_f64 *hq = (const c_f64 *)ka[0];
-            hn[k] = make_double2(hq[2 * (hb + k)], hq[2 * (hb + k) + 1]);
+#ifdef OLPE_DIAG_HSMEM_PW
+            // per wave slot a table of its own (GibbsArgs::diag_h, 64 KiB apart) --
+            // _HALF: 32 rows (512 B), _ROT: a fresh 1 KiB version every sweep (64 of them)
+            {
+              const int slot = (int)blockIdx.x * (int)(blockDim.x >> 6) +
+                               __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+              hq += (size_t)slot * 8192;
+#ifdef OLPE_DIAG_HSMEM_ROT
+              hq += (size_t)(__builtin_amdgcn_readfirstlane(CC ? cc->dver : 0) & 63) * 128;
+#endif
+            }
+#endif
+#ifdef OLPE_DIAG_HSMEM_HALF
+            const int hrw = (hb + k) & 31;
+#else
+            const int hrw = hb + k;
+#endif
+            hn[k] = make_double2(hq[2 * hrw], hq[2 * hrw + 1]);
           }
 #else
           hn[k] = hr[hb + k];
