@@ -664,10 +664,15 @@ def main():
         if steps % 64:
             kms.extend(s.kernel_times(steps % 64))
         km = float(np.mean(kms))
+        # the core clock right after the timed launches (olpe_clock_probe: a 20 us probe
+        # queued on the same stream, outside the timed region): boxes hold different
+        # clocks under this FP64 load, and the roofline fraction at the held clock is
+        # this box's kernel quality
+        clk = s.clock_probe_ghz()
         # every rank's mean sampler time and its own timed-region seconds (one gather, on
         # every rank alike): a scaling shortfall is then attributable from the line --
         # a slow GPU (per_rank_kernel_ms spread) or time outside the sampler kernels
-        per_rank = group.allgather([km, t1 - t0])
+        per_rank = group.allgather([km, t1 - t0, clk])
         return allmax(t1 - t0), km, per_rank
 
     elapsed, kernel_ms, per_rank = measure(args.mode, args.steps, args.warmup)
@@ -678,8 +683,8 @@ def main():
     if world == 1 and not args.no_alt:
         other = "exact" if args.mode == "fast" else "fast"
         alt_steps = max(2, args.steps // 2)
-        e2, k2, _ = measure(other, alt_steps, 1)
-        alt = (other, alt_steps, e2, k2)
+        e2, k2, pr2 = measure(other, alt_steps, 1)
+        alt = (other, alt_steps, e2, k2, pr2[0][2])
 
     def report(elapsed, kernel_ms, units, acceptance, comm, alt=None):
         """rank 0's JSON line (without the CPU baseline)."""
@@ -694,7 +699,7 @@ def main():
         def key(mode):
             return mode if args.config in (2, 3) else f"c{args.config}_{mode}"
 
-        def roofline(mode, kernel_ms):
+        def roofline(mode, kernel_ms, clock_ghz=None):
             """FP64-VALU roofline of the sampler kernel.  frac: executed
             FP64 lane-ops (rocprofv3 SQ counts per walker-step, profiles/valu_counts.json)
             x the live HIP-event walker-step rate / the FP64 vector peak."""
@@ -733,6 +738,11 @@ def main():
                 out.update(achieved=rate * ops / 1e12, frac=rate * ops / FP64_LANE_PEAK,
                            frac_source="operation count (model + chi^2 only; lower bound)",
                            fp64_lane_ops_per_walker_step=ops)
+            if clock_ghz:
+                # this box's clock right after the timed launches, and the fraction of the
+                # FP64 peak at that clock (the peak scales with the clock: 2.4 GHz spec)
+                out["clock_ghz_live"] = clock_ghz
+                out["frac_of_held_clock_live"] = out["frac"] * 2.4 / clock_ghz
             ops = work_per_step(n, nsrc, mode)
             out["model_chi2_frac"] = rate * ops / FP64_LANE_PEAK
             algo = sec8d_work(n, nsrc)
@@ -787,7 +797,7 @@ def main():
                        "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
                                     else "environment" if "WORLD_SIZE" in os.environ
                                     else "none (1 rank)")},
-            "roofline": roofline(args.mode, kernel_ms),
+            "roofline": roofline(args.mode, kernel_ms, per_rank[0][2]),
             "acceptance": acceptance,
             "allgather_ms": None,
         }
@@ -799,6 +809,7 @@ def main():
                                      "ranks": [p[0] for p in per_rank]}
         out["per_rank_elapsed_s"] = {"min": min(p[1] for p in per_rank),
                                      "max": max(p[1] for p in per_rank)}
+        out["per_rank_clock_ghz"] = [p[2] for p in per_rank]
         out["host_overhead_frac"] = 1.0 - kmax * 1e-3 * args.steps / elapsed
         out["host_overhead_note"] = (
             "1 - max over ranks of (mean sampler kernel ms x steps) / the max-over-ranks "
@@ -806,11 +817,11 @@ def main():
             "launch gaps and the host-group barriers")
         out.update(comm)
         if alt:
-            other, alt_steps, e2, k2 = alt
+            other, alt_steps, e2, k2, c2 = alt
             out["alt_eval"] = {"eval": other,
                                "value": world * wpg * args.iters * alt_steps / e2,
                                "ms_per_step": e2 / alt_steps * 1e3,
-                               "roofline": roofline(other, k2)}
+                               "roofline": roofline(other, k2, c2)}
         return out
 
     # end-of-run exchange over RCCL/xGMI, outside the timed region:

@@ -95,6 +95,9 @@ class StubSampler:
     def last_units(self):
         return 1
 
+    def clock_probe_ghz(self):
+        return 2.05
+
     def chain(self):
         return np.broadcast_to(self.state[:, None, :], (self.W, self._nrec, self.ps)).copy()
 

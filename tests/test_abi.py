@@ -148,3 +148,42 @@ def test_kernel_digest_covers_only_the_sampler_bundle():
     assert fatbin_digest(b"no bundles") != ref
     if os.path.exists(LIB):
         assert kernel_digest() == fatbin_digest(_elf_section(LIB, ".hip_fatbin"))
+
+
+def _elf(sections):
+    """A minimal ELF64 little-endian image with the given {name: bytes} sections."""
+    import struct
+    names = [""] + list(sections) + [".shstrtab"]
+    strtab, offs = b"", []
+    for n in names:
+        offs.append(len(strtab))
+        strtab += n.encode() + b"\0"
+    body, places = b"", []
+    for n in names[1:-1]:
+        places.append((64 + len(body), len(sections[n])))
+        body += sections[n]
+    places.append((64 + len(body), len(strtab)))
+    body += strtab
+    shoff = 64 + len(body)
+    hdr = bytearray(64)
+    hdr[:6] = b"\x7fELF\x02\x01"
+    struct.pack_into("<Q", hdr, 0x28, shoff)
+    struct.pack_into("<HHH", hdr, 0x3A, 64, len(names), len(names) - 1)
+    shdrs = bytes(64)
+    for i, (off, size) in enumerate(places):
+        shdrs += struct.pack("<IIQQQQ", offs[i + 1], 1, 0, 0, off, size) + bytes(24)
+    return bytes(hdr) + body + shdrs
+
+
+def test_kernel_digest_hashes_the_code_sections():
+    """Within the sampler's bundle only the code object's code sections count: its
+    symbol table (ordered by the per-build unit ids, __hip_cuid_*, which follow the
+    compile command) may differ without changing the digest; its instructions may not."""
+    from olpefit_amd.build import fatbin_digest
+    m = b"__CLANG_OFFLOAD_BUNDLE__..olpe_gibbs_kernel.."
+    code = {".text": b"\x01\x02\x03\x04" * 8, ".rodata": b"kd" * 8, ".note": b"meta"}
+    a = _elf({**code, ".symtab": b"__hip_cuid_1111111111111111 olpe_gibbs_kernel"})
+    b = _elf({".symtab": b"olpe_gibbs_kernel __hip_cuid_2222222222222222", **code})
+    c = _elf({**code, ".text": b"\x01\x02\x03\x05" * 8, ".symtab": b"x"})
+    assert fatbin_digest(m + a) == fatbin_digest(m + b"pad" + b)
+    assert fatbin_digest(m + a) != fatbin_digest(m + c)

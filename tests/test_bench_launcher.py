@@ -280,6 +280,9 @@ def test_per_rank_kernel_times_and_host_overhead_at_world8():
     assert e["max"] == pytest.approx(elapsed, rel=1e-9) and 0 < e["min"] <= e["max"]
     # the slowest rank sets the step: at least its 34 ms per launch
     assert d["ms_per_step"] >= 34.0
+    # every rank's probed clock, rank 0's beside the roofline
+    assert d["per_rank_clock_ghz"] == pytest.approx([2.05] * 8)
+    assert d["roofline"]["clock_ghz_live"] == pytest.approx(2.05)
 
 
 def test_one_rank_line_carries_the_attribution_fields():
@@ -288,6 +291,9 @@ def test_one_rank_line_carries_the_attribution_fields():
     d = _line(r)
     assert d["per_rank_kernel_ms"]["ranks"] == pytest.approx([20.0])
     assert 0 <= d["host_overhead_frac"] < 1
+    f = d["roofline"]
+    if "frac" in f:
+        assert f["frac_of_held_clock_live"] == pytest.approx(f["frac"] * 2.4 / 2.05)
 
 
 def test_identical_nodes_repeating_bus_ids_are_not_a_shared_gpu():
