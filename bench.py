@@ -414,6 +414,75 @@ def load_json(path: str):
         return None
 
 
+class SmiClock:
+    """The GFX clock the power controller reports for one GPU -- ROCm's amdsmi package
+    (``current_gfxclks``: MHz per XCD, the SMU's metrics table) -- sampled every
+    ``period`` s from a host thread between start() and stop().  It reads the driver's
+    metrics only (no GPU queue, no kernel).  The chip holds its FP64 load below the 2.4 GHz
+    spec clock by an amount that differs from box to box; a probe kernel
+    queued after the launches reads the boost clock the idle chip jumps back to within
+    tens of microseconds, so the clock is sampled while they run."""
+    AMDSMI = "/opt/rocm/share/amd_smi"
+
+    def __init__(self, pci: str, period: float = 0.01):
+        import threading
+        if self.AMDSMI not in sys.path and os.path.isdir(self.AMDSMI):
+            sys.path.append(self.AMDSMI)
+        import amdsmi
+        amdsmi.amdsmi_init()
+        self._smi = amdsmi
+        self._h = next(h for h in amdsmi.amdsmi_get_processor_handles()
+                       if amdsmi.amdsmi_get_gpu_device_bdf(h).lower() == pci.lower())
+        self._read()                                 # fails here if the table is unreadable
+        self.period = period
+        self._samples, self._stop, self._th = [], threading.Event(), None
+
+    def _read(self) -> float:
+        m = self._smi.amdsmi_get_gpu_metrics_info(self._h)
+        v = [x for x in (m.get("current_gfxclks") or [])
+             if isinstance(x, (int, float)) and 0 < x < 10000]
+        if not v and isinstance(m.get("current_gfxclk"), (int, float)):
+            v = [m["current_gfxclk"]]
+        if not v:
+            raise RuntimeError("no GFX clock in the metrics table")
+        return sum(v) / len(v) / 1e3                 # GHz, mean over the XCDs
+
+    def start(self):
+        import threading
+        self._samples, self._stop = [], threading.Event()
+
+        def run():
+            while not self._stop.is_set():
+                try:
+                    self._samples.append(self._read())
+                except Exception:                    # noqa: BLE001 -- a sample lost
+                    pass
+                self._stop.wait(self.period)
+        self._th = threading.Thread(target=run, daemon=True)
+        self._th.start()
+
+    def stop(self):
+        """(mean GHz over the samples, number of samples); (None, 0) if there were none."""
+        self._stop.set()
+        if self._th is not None:
+            self._th.join(timeout=5)
+        n = len(self._samples)
+        return (sum(self._samples) / n if n else None), n
+
+
+def clock_meter(sampler_cls, pci: str):
+    """The clock sampler of this rank's GPU, or None where the metrics are not readable
+    (no amdsmi, no GPU: the line then carries no live clock).  A stand-in sampler class
+    may bring its own (``clock_meter``, tests/bench_stub.py)."""
+    own = getattr(sampler_cls, "clock_meter", None)
+    if own is not None:
+        return own(pci)
+    try:
+        return SmiClock(pci)
+    except Exception:                                # noqa: BLE001
+        return None
+
+
 def sampler_class():
     """The per-GPU sampler, ``olpefit_amd.core.Sampler`` (libolpe.so).  The CPU tests of
     the launcher and of the N > 1 reporting set OLPE_BENCH_SAMPLER=module:Class to a
@@ -635,6 +704,7 @@ def main():
     p0[-1] = s.chi_squared(p0)
     s.seed(odist.walker_seeds(1000, rank * wpg, wpg))      # weak scaling: wpg per GPU
     s.set_state(np.tile(p0, (wpg, 1)))
+    clock = clock_meter(Sampler, placement[rank][4])   # this rank's GPU (its PCI bus id)
 
     def measure(mode, steps, warmup):
         # launches are queued back to back (no host sync between them) and their
@@ -648,6 +718,8 @@ def main():
         barrier()
         s.sync()
         t0 = time.perf_counter()
+        if clock is not None:
+            clock.start()
         kms = []
         for i in range(steps):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
@@ -661,18 +733,15 @@ def main():
         s.sync()
         barrier()
         t1 = time.perf_counter()
+        clk, nclk = clock.stop() if clock is not None else (None, 0)
         if steps % 64:
             kms.extend(s.kernel_times(steps % 64))
         km = float(np.mean(kms))
-        # the core clock right after the timed launches (olpe_clock_probe: a 20 us probe
-        # queued on the same stream, outside the timed region): boxes hold different
-        # clocks under this FP64 load, and the roofline fraction at the held clock is
-        # this box's kernel quality
-        clk = s.clock_probe_ghz()
         # every rank's mean sampler time and its own timed-region seconds (one gather, on
         # every rank alike): a scaling shortfall is then attributable from the line --
         # a slow GPU (per_rank_kernel_ms spread) or time outside the sampler kernels
-        per_rank = group.allgather([km, t1 - t0, clk])
+        # (and the GFX clock the SMU reported over the timed launches, SmiClock)
+        per_rank = group.allgather([km, t1 - t0, clk, nclk])
         return allmax(t1 - t0), km, per_rank
 
     elapsed, kernel_ms, per_rank = measure(args.mode, args.steps, args.warmup)
@@ -810,6 +879,11 @@ def main():
         out["per_rank_elapsed_s"] = {"min": min(p[1] for p in per_rank),
                                      "max": max(p[1] for p in per_rank)}
         out["per_rank_clock_ghz"] = [p[2] for p in per_rank]
+        out["clock_note"] = (
+            "per_rank_clock_ghz / roofline.clock_ghz_live: the GFX clock the SMU reported "
+            "(amdsmi current_gfxclks, mean over the XCDs) sampled every 10 ms over the "
+            f"timed launches ({per_rank[0][3]} samples on rank 0); frac_of_held_clock_live "
+            "= frac x 2.4 GHz / that clock")
         out["host_overhead_frac"] = 1.0 - kmax * 1e-3 * args.steps / elapsed
         out["host_overhead_note"] = (
             "1 - max over ranks of (mean sampler kernel ms x steps) / the max-over-ranks "

@@ -148,11 +148,6 @@ int olpe_last_kernel_ms(olpe_ctx *ctx, double *ms);
 /* Durations of the last n sampler launches (oldest first; n <= 64 and <= launches so
  * far): launches can be queued back to back and timed afterwards. */
 int olpe_kernel_times(olpe_ctx *ctx, int n, double *ms_out);
-/* The core clock (GHz) behind the stream's queued work: a one-wave probe queued on the
- * context's stream counts core cycles over 20 us of the 100 MHz reference; right after
- * sampler launches it reads the clock the chip holds under their load.  Waits for the
- * stream.  Measurement aid; build-specific. */
-int olpe_clock_probe(olpe_ctx *ctx, double *ghz);
 /* Chunks per walker of the last sampler launch (1 = whole walkers; > 1 when the launch
  * cut each walker's iterations into chunks to fill the resident waves).
  * Results do not depend on it.  Build-specific: no reference counterpart. */

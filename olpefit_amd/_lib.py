@@ -62,7 +62,6 @@ SIGNATURES = {
     "olpe_last_kernel_ms": (_i, [_P, _pd]),
     "olpe_kernel_times": (_i, [_P, _i, _pd]),
     "olpe_last_units": (_i, [_P, C.POINTER(C.c_int)]),
-    "olpe_clock_probe": (_i, [_P, _pd]),
     "olpe_unit_stats": (_i, [_P, _pll]),
     "olpe_csv_format": (_i, [_pd, _ll, _i, _i, C.c_char_p, C.c_size_t,
                              C.POINTER(C.c_size_t)]),

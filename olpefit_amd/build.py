@@ -12,7 +12,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libolpe.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("olpe.hip", "olpe_comm.hip", "olpe_moments.hip",
-                                            "olpe_probe.hip", "olpe_csv.cpp")]
+                                            "olpe_csv.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("olpe_device.h", "olpe_internal.h",
                                                  "exp_table.h")] + [
     os.path.join(REPO, "include", "olpe.h")]
@@ -91,8 +91,8 @@ def kernel_digest(lib: str = LIB) -> str:
     hash of the code sections of the built library's code object that holds the sampler
     kernel (its .hip_fatbin section has one clang offload bundle per HIP source: an edit
     to host code, a comment, a diagnostic build's hook, another source's kernels
-    (olpe_moments.hip, olpe_probe.hip) or a change of the compile command's source list
-    leaves it unchanged); without a library, the hash of the flags and the device
+    (olpe_moments.hip) or a change of the compile command's source list leaves it
+    unchanged); without a library, the hash of the flags and the device
     sources' text."""
     import hashlib
     try:

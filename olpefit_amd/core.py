@@ -260,12 +260,6 @@ class Sampler:
         check(self._lib.olpe_unit_stats(self._ctx, out.ctypes.data_as(_lib._pll)))
         return int(out[0]), int(out[1])
 
-    def clock_probe_ghz(self) -> float:
-        """The core clock (GHz) behind the stream's queued work (olpe_clock_probe)."""
-        v = C.c_double(0)
-        check(self._lib.olpe_clock_probe(self._ctx, C.byref(v)))
-        return float(v.value)
-
     def last_units(self) -> int:
         """Chunks per walker of the last sampler launch."""
         v = C.c_int(0)

@@ -1299,8 +1299,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   // olpe_comm_init has nothing to allocate that could fail on one rank while the others
   // wait in ncclCommInitRank
   if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
-      (rc = dev_alloc(&c->d_queue, 4)) || (rc = dev_alloc(&c->d_check, 16)) ||
-      (rc = dev_alloc(&c->d_clk, 4))) {
+      (rc = dev_alloc(&c->d_queue, 4)) || (rc = dev_alloc(&c->d_check, 16))) {
     olpe_destroy(c);
     return rc;
   }
@@ -1355,8 +1354,7 @@ void olpe_destroy(olpe_ctx *c) {
   void *ptrs[] = {c->d_DE, c->d_DW, c->d_state, c->d_tries, c->d_acc,
                   c->d_mt, c->d_mtpos, c->d_gauss, c->d_hasg,  c->d_done,
                   c->d_chain, c->d_trace, c->d_scratch, c->d_scratch2, c->d_queue,
-                  c->d_gather, c->d_uflag, c->d_mmean, c->d_mm2, c->d_mpart, c->d_check,
-                  c->d_clk};
+                  c->d_gather, c->d_uflag, c->d_mmean, c->d_mm2, c->d_mpart, c->d_check};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &pair : c->ev)

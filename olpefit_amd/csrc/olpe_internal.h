@@ -79,7 +79,6 @@ struct olpe_ctx {
   double *d_gather = nullptr;   // receive buffer of olpe_comm_allgather_chain
   size_t gather_cap = 0;
   size_t gather_limit = 0;      // its byte limit (olpe_comm_gather_limit; 0 = none)
-  unsigned long long *d_clk = nullptr;  // clock_probe_kernel's stamps (olpe_clock_probe)
   long long *d_check = nullptr; // the uniformity check's words (allocated by olpe_create,
                                 // so that joining a communicator allocates nothing)
 };

@@ -95,8 +95,15 @@ class StubSampler:
     def last_units(self):
         return 1
 
-    def clock_probe_ghz(self):
-        return 2.05
+    @staticmethod
+    def clock_meter(pci):
+        class Meter:               # (bench.SmiClock's interface: a fixed 2.05 GHz)
+            def start(self):
+                pass
+
+            def stop(self):
+                return 2.05, 3
+        return Meter()
 
     def chain(self):
         return np.broadcast_to(self.state[:, None, :], (self.W, self._nrec, self.ps)).copy()

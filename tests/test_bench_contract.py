@@ -140,3 +140,31 @@ def test_default_workload_names_are_unchanged():
     assert w.startswith(bench.CONFIG_NAMES[2]) and "20 launches x 1000 iterations" in w
     # configs[4]'s shape under --config 2 is custom (the config names the 2-source shape)
     assert bench.workload_name(2, 1, 16384, 128, 3).startswith("custom: ")
+
+
+def test_smi_clock_parses_and_samples_the_metrics_table():
+    """bench.SmiClock: the mean of the valid per-XCD GFX clocks of the SMU's metrics
+    table (MHz -> GHz; 'N/A' and the 65535 filler dropped), sampled from a thread between
+    start() and stop(); clock_meter gives None where no GPU's metrics can be read."""
+    import time
+    import bench
+
+    class FakeSmi:
+        def __init__(self):
+            self.calls = 0
+
+        def amdsmi_get_gpu_metrics_info(self, h):
+            self.calls += 1
+            return {"current_gfxclks": [2000, 2100, 65535, "N/A"], "current_gfxclk": 1}
+
+    c = object.__new__(bench.SmiClock)
+    c._smi, c._h, c.period, c._th = FakeSmi(), None, 0.005, None
+    assert c._read() == pytest.approx(2.05)
+    c.start()
+    time.sleep(0.05)
+    ghz, n = c.stop()
+    assert n >= 2 and ghz == pytest.approx(2.05)
+    c._smi.amdsmi_get_gpu_metrics_info = lambda h: {"current_gfxclks": ["N/A"],
+                                                     "current_gfxclk": 1950}
+    assert c._read() == pytest.approx(1.95)
+    assert bench.clock_meter(object, "0000:ff:00.0") is None      # no such GPU here

@@ -79,9 +79,9 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
     OLPE_UNITS forcing P chunks per walker, each fixture walker's 1,400-5,800
     iterations run as P consecutive chunks on different waves, handed over through
     HBM; every row and accept decision must still equal the reference's loop
-    (apf_step2.py:298-338, 3body :324-373).  Each walker runs as 12 / (walkers)
-    copies, so that the launch has the 12 walkers the 128x128 ring sampler needs before
-    it cuts chunks (a lockstep batch must not hold a chunk and its predecessor).  The
+    (apf_step2.py:298-338, 3body :324-373).  Each walker runs as several copies, so that
+    the launch has at least the 12 walkers the 128x128 ring sampler needs before it cuts
+    chunks (a lockstep batch must not hold a chunk and its predecessor).  The
     ring sampler hands out batches of 12 units to whole workgroups, so 12 walkers are one
     workgroup running its chunks one after the other (hand-offs through HBM without a
     wait); it runs 768 walkers instead -- 64 workgroups, whose chunk-1 batches land on
@@ -92,7 +92,15 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
     g = golden(name)
     nw = len(g["seeds"])
     ring = name.startswith("c128") and mode == "fast"
-    reps = 768 // nw if ring else -(-12 // nw)
+    # the other samplers run ceil(W / WPB) workgroups for so few walkers: with W not a
+    # multiple of the waves per workgroup (12 or 16 at 64x64 and 32x32, 4 for the
+    # L2-resident 128x128 one) the grid has more waves than walkers, and the spare waves'
+    # first units are chunk-1 units whose predecessors are still running -- a hand-off
+    # that waits, by construction (with W a multiple, the waves can finish their chunks in
+    # the order they took them and hand every walker to itself: round 5 saw waits = 0)
+    wpbs = (4,) if name.startswith("c128") else (12, 16)
+    reps = 768 // nw if ring else next(r for r in range(-(-12 // nw), 64)
+                                       if all((nw * r) % b for b in wpbs))
     st = {}
     chain, tr, L = _run(g, mode, reps, st)
     assert st["units"] == units, st

@@ -1296,22 +1296,3 @@ def test_moments_fold_long_launches(golden, lib_loaded, name):
     slack = nrow * (10 * np.finfo(float).eps * np.abs(ref_mean)) ** 2
     assert np.all(np.abs(m2 - ref_m2) <= 1e-10 * np.abs(ref_m2) + slack)
 
-
-def test_clock_probe_reads_a_plausible_core_clock(golden, lib_loaded):
-    """olpe_clock_probe (the bench line's clock_ghz_live): core cycles over 20 us of the
-    100 MHz reference, behind the stream's launches -- a core clock the part can run
-    (MI355X: 2.4 GHz peak), before and after sampler launches, and no effect on them."""
-    g = golden("c32")
-    s = make_sampler(g, "fast")
-    idle = s.clock_probe_ghz()
-    assert 0.1 < idle <= 2.6, idle
-    seeds = np.arange(7, 7 + 64)
-    s.seed(seeds)
-    s.set_state(np.tile(g["p_init"], (64, 1)))
-    a = s.run(200, record_stride=10)
-    busy = s.clock_probe_ghz()
-    assert 0.1 < busy <= 2.6, busy
-    b = make_sampler(g, "fast")
-    b.seed(seeds)
-    b.set_state(np.tile(g["p_init"], (64, 1)))
-    np.testing.assert_array_equal(b.run(200, record_stride=10), a)

@@ -10,7 +10,6 @@ mkdir -p diag/$name
 srcs="$tmp/olpefit_amd/csrc/olpe.hip $tmp/olpefit_amd/csrc/olpe_comm.hip"
 [ -f $tmp/olpefit_amd/csrc/olpe_csv.cpp ] && srcs="$srcs $tmp/olpefit_amd/csrc/olpe_csv.cpp"
 [ -f $tmp/olpefit_amd/csrc/olpe_moments.hip ] && srcs="$srcs $tmp/olpefit_amd/csrc/olpe_moments.hip"
-[ -f $tmp/olpefit_amd/csrc/olpe_probe.hip ] && srcs="$srcs $tmp/olpefit_amd/csrc/olpe_probe.hip"
 /opt/rocm/bin/hipcc $(python -m olpefit_amd.build --print-flags) "$@" \
   -o diag/$name/libolpe.so $srcs -lrccl
 rm -rf $tmp

@@ -5,4 +5,4 @@ name=$1; shift
 mkdir -p diag/$name
 /opt/rocm/bin/hipcc $(python -m olpefit_amd.build --print-flags) \
   "$@" -o diag/$name/libolpe.so olpefit_amd/csrc/olpe.hip olpefit_amd/csrc/olpe_comm.hip \
-  olpefit_amd/csrc/olpe_moments.hip olpefit_amd/csrc/olpe_probe.hip olpefit_amd/csrc/olpe_csv.cpp -lrccl
+  olpefit_amd/csrc/olpe_moments.hip olpefit_amd/csrc/olpe_csv.cpp -lrccl
