@@ -112,10 +112,15 @@ def workload_name(config: int, world: int, wpg: int, n: int | None = None,
 # 1,000 iterations, configs[1] 10,000, configs[2] 2,000, configs[4] 500
 DEFAULTS = {
     0: dict(iters=1000, stride=1, steps=1, warmup=1),
-    1: dict(iters=1000, stride=1, steps=10, warmup=2),
-    2: dict(iters=100, stride=10, steps=20, warmup=5),
-    4: dict(iters=100, stride=10, steps=5, warmup=2),
+    1: dict(iters=1000, stride=1, steps=10, warmup=60),
+    2: dict(iters=100, stride=10, steps=20, warmup=40),
+    4: dict(iters=100, stride=10, steps=5, warmup=35),
 }
+# (warm-up: ~0.5 s of launches before the timed ones.  Same-box A/B, round 5
+# (profiles/r05/warmup/): the timed launches run at the same speed after 2-5 warm-up
+# launches as after 0.5 s, but the power controller's telemetry (SmiClock, the line's
+# clock) still reads low within ~0.3 s of a run's first launch -- configs[1] 1.64-1.70
+# GHz after 2 where 0.5 s of warm-up reads 2.07 -- so the clock is read after it settles)
 DEFAULTS[3] = DEFAULTS[2]
 # BASELINE.json's metric, character for character (its "64\u00d764")
 METRIC = "walker-steps/sec (= model evals/sec) on 64\u00d764 2-source cutout, 1/2/4/8 GPU"
@@ -706,10 +711,14 @@ def main():
     s.set_state(np.tile(p0, (wpg, 1)))
     clock = clock_meter(Sampler, placement[rank][4])   # this rank's GPU (its PCI bus id)
 
+    first_launch = []          # when this rank queued its first sampler launch
+
     def measure(mode, steps, warmup):
         # launches are queued back to back (no host sync between them) and their
         # HIP-event durations read afterwards (olpe_kernel_times)
         s.set_eval_mode(mode)
+        if not first_launch:
+            first_launch.append(time.perf_counter())
         for _ in range(warmup):
             s.run_async(args.iters, burn_in=0, record_stride=args.stride)
             if not args.no_moments:
@@ -740,8 +749,10 @@ def main():
         # every rank's mean sampler time and its own timed-region seconds (one gather, on
         # every rank alike): a scaling shortfall is then attributable from the line --
         # a slow GPU (per_rank_kernel_ms spread) or time outside the sampler kernels
-        # (and the GFX clock the SMU reported over the timed launches, SmiClock)
-        per_rank = group.allgather([km, t1 - t0, clk, nclk])
+        # (and the GFX clock the SMU reported over the timed launches, SmiClock, with the
+        # seconds between this rank's first launch and the timed ones: the telemetry
+        # reads low for ~0.3 s after a run starts)
+        per_rank = group.allgather([km, t1 - t0, clk, nclk, t0 - first_launch[0]])
         return allmax(t1 - t0), km, per_rank
 
     elapsed, kernel_ms, per_rank = measure(args.mode, args.steps, args.warmup)
@@ -753,7 +764,7 @@ def main():
         other = "exact" if args.mode == "fast" else "fast"
         alt_steps = max(2, args.steps // 2)
         e2, k2, pr2 = measure(other, alt_steps, 1)
-        alt = (other, alt_steps, e2, k2, pr2[0][2])
+        alt = (other, alt_steps, e2, k2, pr2[0][2] if pr2[0][4] >= 0.3 else None)
 
     def report(elapsed, kernel_ms, units, acceptance, comm, alt=None):
         """rank 0's JSON line (without the CPU baseline)."""
@@ -866,7 +877,8 @@ def main():
                        "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
                                     else "environment" if "WORLD_SIZE" in os.environ
                                     else "none (1 rank)")},
-            "roofline": roofline(args.mode, kernel_ms, per_rank[0][2]),
+            "roofline": roofline(args.mode, kernel_ms,
+                                 per_rank[0][2] if per_rank[0][4] >= 0.3 else None),
             "acceptance": acceptance,
             "allgather_ms": None,
         }
@@ -879,11 +891,16 @@ def main():
         out["per_rank_elapsed_s"] = {"min": min(p[1] for p in per_rank),
                                      "max": max(p[1] for p in per_rank)}
         out["per_rank_clock_ghz"] = [p[2] for p in per_rank]
+        lead = min(p[4] for p in per_rank)
+        out["clock_settled"] = lead >= 0.3
         out["clock_note"] = (
             "per_rank_clock_ghz / roofline.clock_ghz_live: the GFX clock the SMU reported "
             "(amdsmi current_gfxclks, mean over the XCDs) sampled every 10 ms over the "
-            f"timed launches ({per_rank[0][3]} samples on rank 0); frac_of_held_clock_live "
-            "= frac x 2.4 GHz / that clock")
+            f"timed launches ({per_rank[0][3]} samples on rank 0), which began {lead:.2f} s "
+            "after the first launch; frac_of_held_clock_live = frac x 2.4 GHz / that clock. "
+            "It agrees with the sampler's own s_memtime rate to ~4 % once settled; within "
+            "~0.3 s of a run's first launch the telemetry reads low while the kernels already "
+            "run at full speed (clock_settled false: the roofline's clock fields are then omitted)")
         out["host_overhead_frac"] = 1.0 - kmax * 1e-3 * args.steps / elapsed
         out["host_overhead_note"] = (
             "1 - max over ranks of (mean sampler kernel ms x steps) / the max-over-ranks "
