@@ -482,10 +482,20 @@ def clock_meter(sampler_cls, pci: str):
     own = getattr(sampler_cls, "clock_meter", None)
     if own is not None:
         return own(pci)
-    try:
-        return SmiClock(pci)
-    except Exception:                                # noqa: BLE001
-        return None
+    # (built in a daemon thread with a time limit: a metrics library that blocks must not
+    # hold up the measurement -- the line then simply has no clock)
+    import threading
+    box = []
+
+    def build():
+        try:
+            box.append(SmiClock(pci))
+        except Exception:                            # noqa: BLE001
+            pass
+    th = threading.Thread(target=build, daemon=True)
+    th.start()
+    th.join(timeout=15)
+    return box[0] if box else None
 
 
 def sampler_class():
