@@ -61,9 +61,13 @@ CONFIG_NAMES = {
     0: "configs[0]: 1 walker, 32x32 2-source cutout, 1,000 iterations (plumbing reference)",
     1: "configs[1]: 4,096 walkers, 64x64 2-source cutout, fp64",
     2: "configs[2]: 65,536 walkers/GPU, 64x64 2-source cutout, fp64, LDS-resident image",
-    4: "configs[4]: 3-source 128x128 cutout, 16,384 walkers/GPU, fp64",
+    # (BASELINE configs[4] is 131,072 walkers on 8 GPUs: one GPU runs one shard of it)
+    4: ("configs[4]'s per-GPU shard on 1 GPU (16,384 of 131,072 walkers, 3-source 128x128 "
+        "cutout, fp64; the whole of configs[4] is --gpus 8)"),
 }
 CONFIG3 = ("configs[3]: 524,288 walkers sharded 8 x MI355X (65,536 per GPU, 64x64 2-source "
+           "cutout, fp64), RCCL chain all-gather at the end")
+CONFIG4 = ("configs[4]: 131,072 walkers sharded 8 x MI355X (16,384 per GPU, 3-source 128x128 "
            "cutout, fp64), RCCL chain all-gather at the end")
 
 
@@ -87,13 +91,16 @@ def workload_name(config: int, world: int, wpg: int, n: int | None = None,
                 f"{CONFIGS[config][1]}, {CONFIGS[config][2]} sources)")
     elif config in (2, 3) and world == 8:
         name = CONFIG3
+    elif config == 4 and world == 8:
+        name = CONFIG4
     elif config == 3:
         name = (f"configs[3]'s per-GPU shards on {gpus} ({world} x {wpg:,} of 524,288 "
                 f"walkers; the whole of configs[3] is --gpus 8)")
     elif world > 1:
-        name = (f"{CONFIG_NAMES[config].split(':')[0]}'s shape per GPU, weak-scaled over "
+        name = (f"configs[{config}]'s shape per GPU, weak-scaled over "
                 f"{gpus} ({world} x {wpg:,} walkers, {n}x{n} {nsrc}-source cutout, fp64"
-                + ("; configs[3] is 8 x 65,536)" if config == 2 else ")"))
+                + ("; configs[3] is 8 x 65,536)" if config == 2 else
+                   "; configs[4] is 8 x 16,384)" if config == 4 else ")"))
     else:
         name = CONFIG_NAMES[config]
     d = DEFAULTS[config]
@@ -122,6 +129,8 @@ DEFAULTS = {
 # clock) still reads low within ~0.3 s of a run's first launch -- configs[1] 1.64-1.70
 # GHz after 2 where 0.5 s of warm-up reads 2.07 -- so the clock is read after it settles)
 DEFAULTS[3] = DEFAULTS[2]
+# seconds after a rank's first launch before its SMU clock reading counts as settled
+CLOCK_SETTLE_S = 0.3
 # BASELINE.json's metric, character for character (its "64\u00d764")
 METRIC = "walker-steps/sec (= model evals/sec) on 64\u00d764 2-source cutout, 1/2/4/8 GPU"
 FP64_LANE_PEAK = 78.6e12 / 2      # MI355X FP64 vector: 78.6 TFLOP/s with FMA = 2
@@ -774,7 +783,8 @@ def main():
         other = "exact" if args.mode == "fast" else "fast"
         alt_steps = max(2, args.steps // 2)
         e2, k2, pr2 = measure(other, alt_steps, 1)
-        alt = (other, alt_steps, e2, k2, pr2[0][2] if pr2[0][4] >= 0.3 else None)
+        alt = (other, alt_steps, e2, k2,
+               pr2[0][2] if min(p[4] for p in pr2) >= CLOCK_SETTLE_S else None)
 
     def report(elapsed, kernel_ms, units, acceptance, comm, alt=None):
         """rank 0's JSON line (without the CPU baseline)."""
@@ -887,8 +897,11 @@ def main():
                        "launcher": ("bench.py --gpus" if os.environ.get("OLPE_BENCH_LAUNCHED")
                                     else "environment" if "WORLD_SIZE" in os.environ
                                     else "none (1 rank)")},
+            # (the clock fields only when every rank's telemetry had settled: the same
+            # test as clock_settled below)
             "roofline": roofline(args.mode, kernel_ms,
-                                 per_rank[0][2] if per_rank[0][4] >= 0.3 else None),
+                                 per_rank[0][2] if min(p[4] for p in per_rank) >= CLOCK_SETTLE_S
+                                 else None),
             "acceptance": acceptance,
             "allgather_ms": None,
         }
@@ -902,7 +915,7 @@ def main():
                                      "max": max(p[1] for p in per_rank)}
         out["per_rank_clock_ghz"] = [p[2] for p in per_rank]
         lead = min(p[4] for p in per_rank)
-        out["clock_settled"] = lead >= 0.3
+        out["clock_settled"] = lead >= CLOCK_SETTLE_S
         out["clock_note"] = (
             "per_rank_clock_ghz / roofline.clock_ghz_live: the GFX clock the SMU reported "
             "(amdsmi current_gfxclks, mean over the XCDs) sampled every 10 ms over the "
@@ -950,7 +963,19 @@ def main():
         _quiet_stdout()
         try:
             uid = group.broadcast(Sampler.comm_unique_id() if rank == 0 else None)
+            # the library's own bound on every wait for the other ranks (olpe_comm_timeout:
+            # past it the communicator is aborted and the call raises), inside the
+            # watchdog's, so that a lost peer ends in comm_error rather than the watchdog
+            s.comm_timeout(0.8 * args.comm_timeout)
             s.comm_init(uid, world, rank)
+            # RCCL's own view of the communicator on every rank (ncclCommCount /
+            # ncclCommUserRank), not the arguments it was created with
+            views = group.allgather(list(s.comm_info()))
+            comm["comm"] = {"rccl_nranks": views[0][0],
+                            "rccl_ranks": [v[1] for v in views],
+                            "rccl_nranks_agree": all(v[0] == views[0][0] for v in views)}
+            if views[0][0] != world or [v[1] for v in views] != list(range(world)):
+                raise RuntimeError(f"RCCL sees {views} for a world of {world}")
             barrier()
             tg = time.perf_counter()
             allst = s.allgather_state()
@@ -963,6 +988,8 @@ def main():
                 tm = time.perf_counter()
                 moments = s.allreduce_moments()               # over every rank's walkers
                 comm["moments_allreduce_ms"] = allmax(time.perf_counter() - tm) * 1e3
+                # the walker total the all-reduce summed (slot 1): every rank's walkers
+                comm["comm"]["walkers_allreduced"] = int(moments[1])
             per_walker = s._nrec * s.ps * 8
             wn = max(1, min(wpg, int(args.gather_mib * 2 ** 20 // max(1, per_walker))))
             s.allgather_chain(0, min(wn, wpg), out=False)         # warm-up (buffer, rings)

@@ -206,10 +206,28 @@ int olpe_acceptance_format(const double *x, int n, char *out, size_t cap, size_t
 int olpe_acceptance_write(const char *const *paths, const double *accepts, const double *tries,
                           int nfiles, int np, int threads, unsigned char *done);
 
-/* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) --------------------------------- */
+/* --- multi-GPU (RCCL over xGMI), SURVEY.md §8(e) ---------------------------------
+ * The reference's ranks meet at a per-iteration comm.barrier() (apf_step2.py:338); the
+ * build's ranks meet only in these end-of-run collectives.  No rank is left waiting:
+ * every call first all-reduces a word set (shard sizes, ranges, local failures), and a
+ * rank decides whether to enter the data collective only from that agreed verdict (a
+ * rank whose words cannot reach the device sends a poisoned default that fails the
+ * check everywhere); the moments summary runs both all-reduce rounds on every rank and
+ * decides success from their summed status words.  A failure inside a collective (a dead
+ * peer) is bounded by olpe_comm_timeout: a rank that waits longer aborts its
+ * communicator (OLPE_ECOMM; later collectives OLPE_ESTATE until olpe_comm_init). */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
 int olpe_comm_unique_id(uint8_t *id128);
+/* Join the communicator (non-blocking RCCL set-up, bounded by olpe_comm_timeout: a rank
+ * whose peers never arrive gets OLPE_ECOMM).  RCCL's own rank count and rank are checked
+ * against nranks / rank. */
 int olpe_comm_init(olpe_ctx *ctx, const uint8_t *id128, int nranks, int rank);
+/* Seconds any call may wait for the other ranks (joining, a collective) before it aborts
+ * the communicator and returns OLPE_ECOMM; 0 = no bound.  Default 600.  Build-specific. */
+int olpe_comm_timeout(olpe_ctx *ctx, double seconds);
+/* RCCL's own view of the communicator: ncclCommCount / ncclCommUserRank (OLPE_ESTATE
+ * without one).  Build-specific. */
+int olpe_comm_info(olpe_ctx *ctx, int *nranks, int *rank);
 /* All-gather the walker states of every rank: out [nranks*W][PS] (rank-major; equal W
  * on every rank, checked). */
 int olpe_comm_allgather_state(olpe_ctx *ctx, double *out);
@@ -235,17 +253,14 @@ int olpe_comm_gather_limit(olpe_ctx *ctx, long long bytes);
  * walkers, with centre = the pooled mean (out[2 + k] / out[1]).  Every rank must have
  * folded the same number of rows (checked: OLPE_EINVAL on every rank otherwise); the
  * walker counts may differ (a sum needs no equal shards).
- * Without olpe_comm_init it summarises this context alone.  Hang-free by construction:
- * every local allocation (and the zeroing of unfolded moments) happens before the
- * uniformity check and its failure travels in it (OLPE_ENOMEM on every rank); past the
- * check every rank enters both all-reduces whatever its local summary did, a failure
- * summed into a status word, so all ranks return an error together (this rank's own, or
- * OLPE_ECOMM naming how many other ranks failed). */
+ * Without olpe_comm_init it summarises this context alone.  Every local allocation (and
+ * the zeroing of unfolded moments) happens before the uniformity check and its failure
+ * travels in it (OLPE_ENOMEM on every rank); past the check every rank enters both
+ * all-reduces whatever happened locally, a failure summed into a status word, so all
+ * ranks return an error together (this rank's own, or OLPE_ECOMM naming how many other
+ * ranks failed) -- except a rank that fails only to read round 2's sums back, which
+ * returns its own error while its peers succeed. */
 int olpe_comm_allreduce_moments(olpe_ctx *ctx, double *out);
-/* Test hook for the failure paths of the moments summary: where = 1 makes the
- * preparation's allocation fail (OLPE_ENOMEM before any collective), 2 makes the local
- * summary launch fail (after the uniformity check), 0 clears.  Build-specific. */
-int olpe_moments_fault(olpe_ctx *ctx, int where);
 
 /* --- whole-run posterior moments ----------------------------
  * apf_step3.py reads every chain file (:169-186) to compute per-parameter means, sigmas

@@ -32,7 +32,8 @@ _pu32 = C.POINTER(C.c_uint32)
 _pu8 = C.POINTER(C.c_uint8)
 _pll = C.POINTER(C.c_longlong)
 
-#: name -> (restype, argtypes); mirrors include/olpe.h one-to-one
+#: name -> (restype, argtypes); mirrors include/olpe.h and the test hooks of
+#: include/olpe_test.h one-to-one
 SIGNATURES = {
     "olpe_version": (_i, []),
     "olpe_device_count": (_i, [C.POINTER(_i)]),
@@ -78,11 +79,14 @@ SIGNATURES = {
     "olpe_moments_summary": (_i, [_P, _pd, _pd]),
     "olpe_comm_unique_id": (_i, [_pu8]),
     "olpe_comm_init": (_i, [_P, _pu8, _i, _i]),
+    "olpe_comm_timeout": (_i, [_P, _d]),
+    "olpe_comm_info": (_i, [_P, C.POINTER(_i), C.POINTER(_i)]),
     "olpe_comm_allgather_state": (_i, [_P, _pd]),
     "olpe_comm_allgather_chain": (_i, [_P, _ll, _ll, _pd, _pll]),
     "olpe_comm_gather_limit": (_i, [_P, _ll]),
     "olpe_comm_allreduce_moments": (_i, [_P, _pd]),
     "olpe_moments_fault": (_i, [_P, _i]),
+    "olpe_test_hold_handoff": (_i, [_P, _i]),
 }
 
 _lib = None

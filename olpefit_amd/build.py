@@ -14,8 +14,8 @@ LIB = os.path.join(HERE, "libolpe.so")
 SOURCES = [os.path.join(CSRC, f) for f in ("olpe.hip", "olpe_comm.hip", "olpe_moments.hip",
                                             "olpe_csv.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("olpe_device.h", "olpe_internal.h",
-                                                 "exp_table.h")] + [
-    os.path.join(REPO, "include", "olpe.h")]
+                                                 "exp_table.h", "olpe_comm_proto.h")] + [
+    os.path.join(REPO, "include", h) for h in ("olpe.h", "olpe_test.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17",
          # numpy evaluates a*b + c as two rounded ops; keep that order in the

@@ -292,6 +292,17 @@ class Sampler:
         check(self._lib.olpe_comm_init(self._ctx, buf, nranks, rank))
         self.nranks = nranks
 
+    def comm_timeout(self, seconds: float):
+        """Bound on any wait for the other ranks (olpe_comm_timeout; 0 = none): past it
+        the communicator is aborted and the call raises (OLPE_ECOMM)."""
+        check(self._lib.olpe_comm_timeout(self._ctx, float(seconds)))
+
+    def comm_info(self) -> tuple[int, int]:
+        """RCCL's own (rank count, rank) of this context's communicator."""
+        n, r = C.c_int(-1), C.c_int(-1)
+        check(self._lib.olpe_comm_info(self._ctx, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
     def allgather_state(self):
         out = np.empty((self.nranks * self.W, self.ps))
         check(self._lib.olpe_comm_allgather_state(self._ctx, _dptr(out)))
@@ -320,9 +331,17 @@ class Sampler:
         check(self._lib.olpe_comm_allreduce_moments(self._ctx, _dptr(out)))
         return out
 
+    def hold_handoff(self, on: bool = True):
+        """Test hook (olpe_test_hold_handoff, include/olpe_test.h): chunked launches hold
+        each first chunk's hand-off until a later chunk is waiting for one, so a hand-off
+        wait happens by construction (olpe_unit_stats counts it)."""
+        check(self._lib.olpe_test_hold_handoff(self._ctx, 1 if on else 0))
+
     def moments_fault(self, where: int):
-        """Test hook (olpe_moments_fault): 1 = the summary's allocation fails, 2 = its
-        launch fails after the uniformity check, 0 = clear."""
+        """Test hook (olpe_moments_fault, include/olpe_test.h): 1 = the summary's
+        allocation fails, 2 = its launch fails after the uniformity check, 3 = the check
+        words fail to reach the device (every collective), 4 = round 1's sums fail to come
+        back, 0 = clear."""
         check(self._lib.olpe_moments_fault(self._ctx, int(where)))
 
     # -- whole-run moments (SURVEY.md §8(f) row 1) ---------------------------------

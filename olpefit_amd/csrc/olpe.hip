@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/olpe.h"
+#include "../../include/olpe_test.h"
 #include "olpe_device.h"
 #include "olpe_internal.h"
 
@@ -48,11 +49,6 @@ template <int NSRC> __device__ __forceinline__ double width_of(int r) {
 }
 
 struct GibbsArgs {
-#ifdef OLPE_DIAG_HSMEM_PW
-  // (diagnostic build only, first so that it sits at kernarg offset 0 where the
-  // OLPE_DIAG_HSMEM hook reads its table base: 64 KiB of finite doubles per wave slot)
-  const double *diag_h;
-#endif
   const double2 *DE;   // [n*n] {data, 1/err} (EXACT) or {data/err, 1/err} (FAST); {0,0} masked
   int n;
   int bkgd_mode;
@@ -92,26 +88,17 @@ struct GibbsArgs {
   int stagger;         // start offset per wave rank within a SIMD, in ~0.5 us: always 0
                        // (round 2's OLPE_STAGGER changed nothing; the host knob is gone,
                        // the argument kept so that the sampler's code is unchanged)
+  unsigned *hold;      // test hook (olpe_test_hold_handoff), null otherwise: a wave that
+                       // ends a walker's first chunk waits, before it hands the walker on,
+                       // until a wave waiting for some walker's next chunk sets the word --
+                       // so every launch with chunks has a hand-off that waits, whatever
+                       // the dispatch order (verdict r05 item 5)
 };
 
 constexpr int kTraceF = 6;
 // sampler LDS header: the exp table, then 64 B of progress-balancing words
 constexpr int kSampHdr = kEtabBytes + 64;
 
-// Diagnostic build only (tools/diag_build.sh ... -DOLPE_DIAG_TIMING): per-wave cycle
-// totals of the step's sections (s_memtime), written over the trace buffer at the end.
-#ifdef OLPE_DIAG_TIMING
-#define DT_MARK(i)                                             \
-  do {                                                         \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    dt[i] += _t - dt_last;                                     \
-    dt_last = _t;                                              \
-  } while (0)
-#else
-#define DT_MARK(i) \
-  do {             \
-  } while (0)
-#endif
 
 // ---------------------------------------------------------------------------------
 // The fused sampler
@@ -168,7 +155,7 @@ __host__ __device__ constexpr int sampler_vtab_bytes(int n, int nsrc, int nt, in
 template <int NP> __host__ __device__ constexpr int ring_wave_bytes(int n) {
   return WaveSlice<NP>::OPE + kDrawTabBytes + 2 * n * 16;
 }
-// (8 waves: the OLPE_DIAG_RING8 diagnostic build only -- the same sweep at 2 waves per
+// (8 waves: the diagnostic 8-wave ring of tools/diag/diag_hooks.patch only -- the same sweep at 2 waves per
 // SIMD, the bound on the 4-wave layout's gain)
 __host__ __device__ constexpr bool ring_wpb(int nt, int wpb) {
   return nt == 128 && (wpb == 12 || wpb == 8);
@@ -240,13 +227,16 @@ __device__ __forceinline__ void unit_publish(unsigned *flag, unsigned v, int lan
 }
 __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigned *err,
                                           unsigned long long *stats, int lane,
-                                          unsigned long long limit) {
+                                          unsigned long long limit, unsigned *hold) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool waited = false;
   for (;;) {
     const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load((gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (v == want) break;
+    // (test hook: this wait releases the first chunks held at their hand-off)
+    if (!waited && hold && lane == 0)
+      __hip_atomic_store((gu32 *)hold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     waited = true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
       __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -263,6 +253,20 @@ __device__ __forceinline__ void unit_wait(unsigned *flag, unsigned want, unsigne
   // earlier chunk
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// test hook (olpe_test_hold_handoff): hold a first chunk's hand-off until some wave is
+// waiting for a hand-off (bounded like unit_wait: the grid always drains)
+__device__ __forceinline__ void hold_handoff(unsigned *hold, unsigned *err, unsigned long long limit) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_readfirstlane((int)__hip_atomic_load((gu32 *)hold, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+      __hip_atomic_store((gu32 *)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
 }
 
 // wave priority of the step's control chain (the sweep runs at 0, or 0/1 with balancing)
@@ -400,7 +404,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       // the walker's previous chunk ran on another wave: wait for its hand-off
       if (k > 0 && active)
         unit_wait(K()->uflag + w, K()->utag + (unsigned)k, K()->uerr, K()->queue + 2, lane,
-                  K()->wait_ticks);
+                  K()->wait_ticks, K()->hold);
     }
     // ring sampler: the batch's waves run max(it_e - it_s) lockstep steps; a wave past
     // its own iterations (or without a unit) keeps the phase barriers (idle steps)
@@ -413,10 +417,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       it_end = it_s + (int)__builtin_amdgcn_readfirstlane((int)mx);
       if (!active) it_e = it_s;
     }
-#ifdef OLPE_DIAG_SPAN
-    const unsigned long long span_t0 = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long span_c0 = __builtin_amdgcn_s_memtime();
-#endif
     // ---- walker state -> LDS slice
     if (lane < NP) {
       s_tries[lane] = K()->tries[(size_t)w * NP + lane];
@@ -475,10 +475,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
     ccache.pbuf = reinterpret_cast<double *>(wb + WS::OPE);
     ccache.colc = colc;
     __builtin_amdgcn_s_setprio(kCtrlPrio);
-#ifdef OLPE_DIAG_TIMING
-    unsigned long long dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long dt_last = __builtin_amdgcn_s_memtime();
-#endif
     for (int it = it_s; it < it_end; ++it) {
       if constexpr (RING) {
         if (it >= it_e) {
@@ -499,7 +495,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       if (A.accept_min > 0 && tr == (uint32_t)A.accept_min) {
         if (++ndone == NP && done_at < 0) done_at = A.count0 + it + 1;
       }
-      DT_MARK(0);
 
       // proposal / logproposal (:63-70, :306-309): loc + scale*gauss
       // (read by every lane: nv is made uniform below, cur needs no readfirstlane)
@@ -536,7 +531,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         nv = cur + wr * g;
       }
       nv = uniform_f64(nv);
-      DT_MARK(1);
 
       // coefficient sets of the proposal: only the set that r touches is rebuilt
       auto q = [&](int k) -> double { return (k == r) ? nv : st[k]; };
@@ -597,7 +591,6 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         mdl->bg = q(A.bkgd_mode == 0 ? L::BG_QUIRK : L::BG_FIXED);
       }
       wave_sync();
-      DT_MARK(2);
 
       // build_analytical_model + chi_squared (:314-316)
       // the step's scalar control is a latency-bound chain: it runs at raised wave
@@ -642,11 +635,9 @@ void olpe_gibbs_kernel(GibbsArgs A) {
                                                      RING ? &ring : nullptr);
       }
       __builtin_amdgcn_s_setprio(kCtrlPrio);
-      DT_MARK(3);
       // (the total is valid in lane 63: the accept ballots that lane's test, and lane 63
       // stores an accepted chi^2, so the step needs no readlanes of the sum)
       const double chi = wave_sum_v(part);
-      DT_MARK(4);
 
       // accept_reject (:139-148): EXACT dice < exp(-(chi - cur)/2); FAST the same test
       // as chi - cur < -2 log(dice) against the batch's threshold table (a NaN chi^2
@@ -689,9 +680,7 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         }
       }
       wave_sync();
-      DT_MARK(5);
 
-#if !defined(OLPE_DIAG_TIMING) && !defined(OLPE_DIAG_SPAN)
       if (A.trace) {
        if (lane == 0) {
         double *t = A.trace + ((size_t)w * A.n_iters + it) * kTraceF;
@@ -703,36 +692,14 @@ void olpe_gibbs_kernel(GibbsArgs A) {
         t[5] = acc ? 1.0 : 0.0;
        }
       }
-#endif
       // chain record (:342-351, generalised to a stride)
       if (it == rec_it) {
         if (rec_row >= 0 && rec_row < nrows && lane < PS) chain_w[rec_row * PS + lane] = st[lane];
         rec_it += rstride;
         ++rec_row;
       }
-      DT_MARK(6);
     }
-#ifdef OLPE_DIAG_TIMING
-    if (A.trace && lane < 9) {
-      unsigned long long v = lane == 7 ? ccache.n_setup : lane == 8 ? ccache.n_refresh : 0;
-      if constexpr (RING) v = lane == 7 ? ring.wait_first : lane == 8 ? ring.wait_rest : v;
-      for (int k = 0; k < 7; ++k) v = (lane == k) ? dt[k] : v;
-      A.trace[(size_t)w * A.n_iters * kTraceF + lane] = (double)v;
-    }
-#endif
 
-#ifdef OLPE_DIAG_SPAN
-    // diagnostic build only: the unit's start / end (100 MHz), HW_ID and XCC_ID in the trace
-    if (A.trace && lane < 5) {
-      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
-      const double v = lane == 0 ? (double)span_t0 : lane == 1 ? (double)t1
-                     : lane == 2 ? (double)hw : lane == 3 ? (double)xcc : (double)(c1 - span_c0);
-      A.trace[(size_t)w * A.n_iters * kTraceF + 5 * k + lane] = v;
-    }
-#endif
     // ---- write back (the walker index laundered: its per-lane addresses are
     // recomputed here, not kept live across the sampler loop from the loads above)
     wave_sync();
@@ -753,7 +720,10 @@ void olpe_gibbs_kernel(GibbsArgs A) {
       st_wt(K()->done_at + w, done_at);
     }
     // hand the walker to the wave that takes its next chunk
-    if (k < K()->units - 1) unit_publish(K()->uflag + w, K()->utag + (unsigned)(k + 1), lane);
+    if (k < K()->units - 1) {
+      if (k == 0 && K()->hold) hold_handoff(K()->hold, K()->uerr, K()->wait_ticks);
+      unit_publish(K()->uflag + w, K()->utag + (unsigned)(k + 1), lane);
+    }
     wave_sync();      // the slice is reused by the wave's next walker
     if constexpr (!RING) u = K()->queue ? take() : INT_MAX;
   }
@@ -956,12 +926,6 @@ size_t lds_bytes(const olpe_ctx *c, int wpb, bool ring = false) {
   return b;
 }
 
-#ifdef OLPE_DIAG_HSMEM_PW
-__global__ void diag_fill_kernel(double2 *out, size_t n, const double2 *src, size_t npix) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = src[i % npix];
-}
-#endif
 
 template <int NSRC, int NT, bool LDS, int WPB, bool FAST>
 int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
@@ -986,6 +950,7 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
   q.utag = 0;
   q.uerr = reinterpret_cast<unsigned *>(c->d_queue + 1);
   q.stagger = c->stagger;
+  q.hold = nullptr;
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WPB * 64, shm));
   const unsigned resident = (unsigned)std::max(1, per_cu) * (unsigned)c->n_cu;
@@ -1007,6 +972,18 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
     q.units = units;
     c->utag += 16;
     q.utag = c->utag;
+    if (c->hold_handoff && units > 1) {
+      // test hook: one workgroup more than the first chunks need, so that some wave's
+      // first unit is a later chunk whose predecessor is held -- it must wait, and its
+      // wait releases the hold.  Every workgroup must be resident for that.
+      const unsigned need = (unsigned)((a.W + WPB - 1) / WPB) + 1;
+      if (need > resident)
+        return set_err(OLPE_EINVAL, "olpe_test_hold_handoff: %lld walkers need %u resident "
+                       "workgroups, the device holds %u", a.W, need, resident);
+      blocks = need;
+      HIPCHK(hipMemsetAsync(c->d_queue + 4, 0, sizeof(unsigned long long), c->stream));
+      q.hold = reinterpret_cast<unsigned *>(c->d_queue + 4);
+    }
   }
   // progress balancing (olpe_gibbs_kernel): on by default for a 16-wave 2-source FAST
   // launch that runs its walkers whole in one round, which ends on its slowest wave
@@ -1027,26 +1004,6 @@ int launch_gibbs_t(olpe_ctx *c, const GibbsArgs &a) {
                        : (unsigned long long)std::min(std::max(ticks, 3e9), 1e15);
     c->wait_limit_s = (double)q.wait_ticks * 1e-8;
   }
-#ifdef OLPE_DIAG_HSMEM_PW
-  {
-    // (diagnostic build only: a 64 KiB region per wave slot, the cutout repeated)
-    static double *diag_buf = nullptr;
-    static size_t diag_cap = 0;
-    const size_t need = (size_t)blocks * WPB * 65536;
-    if (need > diag_cap) {
-      if (diag_buf) (void)hipFree(diag_buf);
-      diag_buf = nullptr;
-      diag_cap = 0;
-      HIPCHK(hipMalloc((void **)&diag_buf, need));
-      diag_cap = need;
-      const size_t n2 = need / 16, npix = (size_t)a.n * a.n;
-      hipLaunchKernelGGL(diag_fill_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0,
-                         c->stream, reinterpret_cast<double2 *>(diag_buf), n2, a.DE, npix);
-      HIPCHK(hipGetLastError());
-    }
-    q.diag_h = diag_buf;
-  }
-#endif
   hipLaunchKernelGGL(k, dim3(blocks), dim3(WPB * 64), shm, c->stream, q);
   HIPCHK(hipGetLastError());
   // the launch takes W * units + (its waves) values off the counter (the ring sampler:
@@ -1097,9 +1054,6 @@ template <int NSRC, bool FAST> int launch_gibbs_m(olpe_ctx *c, const GibbsArgs &
       // (two 6-wave workgroups per CU with rings of their own -- their control phases
       // apart -- ran at 0.65x: the dispatcher does not pack two of them on a CU)
       if (c->ring_wpb && c->queue_on && c->d_queue && c->d_uflag) {
-#ifdef OLPE_DIAG_RING8
-        if (c->ring_wpb == 8) return launch_gibbs_t<NSRC, 128, false, 8, FAST>(c, a);
-#endif
         return launch_gibbs_t<NSRC, 128, false, 12, FAST>(c, a);
       }
     }
@@ -1150,13 +1104,6 @@ extern "C" {
 
 int olpe_version(void) { return 101; }
 
-#ifdef OLPE_DIAG_FALLBACK
-// diagnostic build only: the sweep-kind counters of olpe_device.h (tools/diag_fallback.py)
-int olpe_diag_fallback(unsigned long long *out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_fb), 4 * sizeof(unsigned long long)) ==
-                 hipSuccess ? OLPE_OK : OLPE_EHIP;
-}
-#endif
 
 const char *olpe_last_error(void) { return g_err; }
 
@@ -1295,17 +1242,16 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   for (auto &pair : c->ev)
     for (auto &ev : pair)
       if (hipEventCreate(&ev) != hipSuccess) ev = nullptr;
-  // d_check: the RCCL uniformity check's words (olpe_comm.hip), allocated here so that
-  // olpe_comm_init has nothing to allocate that could fail on one rank while the others
-  // wait in ncclCommInitRank
+  // the collectives' words (olpe_comm_setup), allocated here so that olpe_comm_init has
+  // nothing to allocate that could fail on one rank while the others wait for it
   if ((rc = dev_alloc(&c->d_DE, npix)) || (rc = dev_alloc(&c->d_DW, npix)) ||
-      (rc = dev_alloc(&c->d_queue, 4)) || (rc = dev_alloc(&c->d_check, 16))) {
+      (rc = dev_alloc(&c->d_queue, 5)) || (rc = olpe_comm_setup(c))) {
     olpe_destroy(c);
     return rc;
   }
   // [0] the queue counter, [1] the hand-off error word, [2..3] hand-off statistics
-  // (unit_wait)
-  if (hipMemset(c->d_queue, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+  // (unit_wait), [4] the hand-off hold word (olpe_test_hold_handoff)
+  if (hipMemset(c->d_queue, 0, 5 * sizeof(unsigned long long)) != hipSuccess ||
       hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) !=
           hipSuccess || c->n_cu <= 0) {
     olpe_destroy(c);
@@ -1322,12 +1268,7 @@ int olpe_create(const void *image, int image_dtype, const void *pois2, double re
   }
   if (const char *e = getenv("OLPE_RING")) {                                // A/B, tests
     const int v = atoi(e);
-#ifdef OLPE_DIAG_RING8
-    const bool diag8 = v == 8;      // diagnostic build: the 8-wave ring (2 waves per SIMD)
-#else
-    const bool diag8 = false;
-#endif
-    if (v != 0 && v != 12 && !diag8) {
+    if (v != 0 && v != 12) {
       olpe_destroy(c);
       return set_err(OLPE_EINVAL, "OLPE_RING=%s: must be 0 (off) or 12 (waves per workgroup)", e);
     }
@@ -1705,6 +1646,12 @@ int olpe_rng_stream(olpe_ctx *c, int kind, int n, void *out) {
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d);
   if (e != hipSuccess) return set_err(OLPE_EHIP, "rng stream: %s", hipGetErrorString(e));
+  return OLPE_OK;
+}
+
+int olpe_test_hold_handoff(olpe_ctx *c, int on) {
+  if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
+  c->hold_handoff = on != 0;
   return OLPE_OK;
 }
 

@@ -9,32 +9,38 @@
 //   * the posterior summary from the whole-run moments (olpe_moments.hip): two
 //     all-reduces (sum) -- the pooled mean, then the walkers' deviations about it
 // The reference's equivalent is one chain file per MPI rank behind the lockstep
-// barrier (apf_step2.py:338, :355-360).  RCCL gathers need equal counts on every rank:
-// each collective first all-reduces {W, -W, rows, -rows, range, -range, bad, alloc}
-// (max) and returns OLPE_EINVAL / OLPE_ENOMEM on every rank when the shards or the
-// requested ranges differ, a range is invalid or an allocation failed on some rank,
-// instead of hanging or mixing rows.
+// barrier (apf_step2.py:338, :355-360).
+//
+// Which rank enters which collective is decided by the protocol in olpe_comm_proto.h
+// (shared with the CPU tests' N-thread world); this file is its RCCL backend:
+//   * the communicator is non-blocking (ncclConfig_t::blocking = 0), so that joining it
+//     and every wait on it is bounded: a rank that waits longer than olpe_comm_timeout
+//     (default 600 s) for its peers -- one that never arrives at ncclCommInitRank, or a
+//     collective a dead peer never enters -- aborts its communicator (ncclCommAbort) and
+//     returns OLPE_ECOMM instead of hanging;
+//   * the uniformity check's words and the poisoned defaults a rank sends when its own
+//     words cannot reach the device live in one buffer allocated with the context.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../include/olpe.h"
+#include "../../include/olpe_test.h"
+#include "olpe_comm_proto.h"
 #include "olpe_internal.h"
 
 using olpe::set_err;
+namespace proto = olpe::proto;
 
 namespace {
 
-#define NCCLCHK(expr)                                                                   \
-  do {                                                                                  \
-    ncclResult_t r_ = (expr);                                                           \
-    if (r_ != ncclSuccess)                                                              \
-      return set_err(OLPE_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(r_));      \
-  } while (0)
 #define HIPCHK(expr)                                                                    \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
@@ -42,13 +48,198 @@ namespace {
       return set_err(OLPE_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
   } while (0)
 
+// the context's comm buffer (olpe_comm_setup): check words | i64 poison | f64 poison
+constexpr size_t kPoisonI64Off = 16, kPoisonF64Off = 32;
+static_assert(proto::kCheckWords <= 16, "check words fit their slot");
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Abort the communicator (every later collective of this context is OLPE_ESTATE until a
+// new olpe_comm_init), drain the stream the aborted collective ran on, return OLPE_ECOMM.
+int abort_comm(olpe_ctx *c, const char *fmt, ...) {
+  char msg[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  if (c->comm) (void)ncclCommAbort((ncclComm_t)c->comm);
+  c->comm = nullptr;
+  c->comm_aborted = true;
+  // the aborted kernels see RCCL's abort flag and exit; bounded all the same
+  const double t0 = now_s();
+  while (hipStreamQuery(c->stream) == hipErrorNotReady && now_s() - t0 < 10.0)
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  (void)hipGetLastError();
+  return set_err(OLPE_ECOMM, "%s", msg);
+}
+
+// pause between polls: spin briefly (a collective of the end-of-run exchange usually
+// completes in microseconds to milliseconds), then sleep
+void poll_pause(int &spins) {
+  if (++spins < 2000)
+    std::this_thread::yield();
+  else
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+}
+
+// An RCCL call on the non-blocking communicator: ncclInProgress means it completes in
+// the background -- poll the communicator's state, bounded by the timeout.
+int settle(olpe_ctx *c, ncclResult_t r, const char *what) {
+  if (r == ncclSuccess) return OLPE_OK;
+  if (r != ncclInProgress) {
+    if (c->comm) return abort_comm(c, "%s: %s", what, ncclGetErrorString(r));
+    return set_err(OLPE_ECOMM, "%s: %s", what, ncclGetErrorString(r));
+  }
+  const double t0 = now_s();
+  int spins = 0;
+  for (;;) {
+    ncclResult_t a = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError((ncclComm_t)c->comm, &a);
+    if (q != ncclSuccess) return abort_comm(c, "%s: ncclCommGetAsyncError: %s", what,
+                                            ncclGetErrorString(q));
+    if (a == ncclSuccess) return OLPE_OK;
+    if (a != ncclInProgress) return abort_comm(c, "%s: %s", what, ncclGetErrorString(a));
+    if (c->comm_timeout_s > 0 && now_s() - t0 > c->comm_timeout_s)
+      return abort_comm(c, "%s: the other ranks did not answer within %g s (olpe_comm_timeout): "
+                        "communicator aborted", what, c->comm_timeout_s);
+    poll_pause(spins);
+  }
+}
+
+// Wait for the context's stream.  With a communicator the wait is bounded by the timeout
+// and watches RCCL's asynchronous errors: a collective whose peers never come (a rank
+// that died or left) ends in an abort here, not in a hang.
+int comm_wait(olpe_ctx *c, const char *what) {
+  if (!c->comm) {
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? OLPE_OK : set_err(OLPE_EHIP, "%s: %s", what, hipGetErrorString(e));
+  }
+  const double t0 = now_s();
+  int spins = 0;
+  for (;;) {
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) return OLPE_OK;
+    if (e != hipErrorNotReady) return set_err(OLPE_EHIP, "%s: %s", what, hipGetErrorString(e));
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError((ncclComm_t)c->comm, &a) == ncclSuccess && a != ncclSuccess &&
+        a != ncclInProgress)
+      return abort_comm(c, "%s: RCCL reported %s", what, ncclGetErrorString(a));
+    if (c->comm_timeout_s > 0 && now_s() - t0 > c->comm_timeout_s)
+      return abort_comm(c, "%s: still waiting for the other ranks after %g s "
+                        "(olpe_comm_timeout): communicator aborted", what, c->comm_timeout_s);
+    poll_pause(spins);
+  }
+}
+
+// The RCCL backend of olpe_comm_proto.h.  Without a communicator (the moments summary
+// of one context) the collectives are copies.
+struct Rccl {
+  olpe_ctx *c;
+  // (an aborted communicator is still a communicator: its collectives fail, they do not
+  // turn into local copies)
+  bool has_comm() const { return c->comm != nullptr || c->comm_aborted; }
+  int aborted(proto::Site s) const {
+    return set_err(OLPE_ECOMM, "%s: the communicator was aborted earlier in this call",
+                   proto::site_name(s));
+  }
+  // test hook (olpe_moments_fault 3 / 4): the step fails as a HIP error would
+  bool forced(proto::Site s) const {
+    return (c->mom_fault == 3 && s == proto::kCheckSend) ||
+           (c->mom_fault == 4 && s == proto::kR1Back);
+  }
+  int fail(proto::Site s) const {
+    return set_err(OLPE_EHIP, "%s: failure forced (olpe_moments_fault)", proto::site_name(s));
+  }
+  int copy(void *dst, const void *src, size_t n, hipMemcpyKind kind, proto::Site s) {
+    if (forced(s)) return fail(s);
+    const hipError_t e = hipMemcpyAsync(dst, src, n, kind, c->stream);
+    return e == hipSuccess ? OLPE_OK
+                           : set_err(OLPE_EHIP, "%s: %s", proto::site_name(s), hipGetErrorString(e));
+  }
+  int h2d(void *d, const void *h, size_t n, proto::Site s) {
+    return copy(d, h, n, hipMemcpyHostToDevice, s);
+  }
+  int d2h(void *h, const void *d, size_t n, proto::Site s) {
+    return copy(h, d, n, hipMemcpyDeviceToHost, s);
+  }
+  template <class T>
+  int reduce(const T *send, T *recv, size_t n, ncclDataType_t t, ncclRedOp_t op, proto::Site s) {
+    if (c->comm_aborted) return aborted(s);
+    if (!c->comm) return send == recv ? OLPE_OK : copy(recv, send, n * sizeof(T),
+                                                       hipMemcpyDeviceToDevice, s);
+    return settle(c, ncclAllReduce(send, recv, n, t, op, (ncclComm_t)c->comm, c->stream),
+                  proto::site_name(s));
+  }
+  int allreduce_max_i64(const long long *s, long long *r, size_t n, proto::Site site) {
+    return reduce(s, r, n, ncclInt64, ncclMax, site);
+  }
+  int allreduce_sum_f64(const double *s, double *r, size_t n, proto::Site site) {
+    return reduce(s, r, n, ncclDouble, ncclSum, site);
+  }
+  int allgather_f64(const double *s, double *r, size_t n, proto::Site site) {
+    if (c->comm_aborted) return aborted(site);
+    if (!c->comm) return copy(r, s, n * sizeof(double), hipMemcpyDeviceToDevice, site);
+    return settle(c, ncclAllGather(s, r, n, ncclDouble, (ncclComm_t)c->comm, c->stream),
+                  proto::site_name(site));
+  }
+  int wait(proto::Site s) {
+    if (forced(s)) {
+      (void)comm_wait(c, proto::site_name(s));
+      return fail(s);
+    }
+    return comm_wait(c, proto::site_name(s));
+  }
+  int local_summary(const double *dcen, double *d, proto::Site) {
+    return olpe_moments_local(c, dcen, d);
+  }
+  long long *check_words() { return c->d_check; }
+  const long long *poison_i64() { return c->d_check + kPoisonI64Off; }
+  const double *poison_f64() { return reinterpret_cast<const double *>(c->d_check + kPoisonF64Off); }
+};
+
 }  // namespace
 
-void olpe_comm_release(olpe_ctx *c) {
-  if (c && c->comm) {
-    (void)ncclCommDestroy((ncclComm_t)c->comm);
-    c->comm = nullptr;
+// The context's comm buffer, allocated and filled by olpe_create (so that joining a
+// communicator allocates nothing that could fail on one rank while the others wait in
+// ncclCommInitRank): the check words, then the poisoned defaults -- i64: zeros with kLost
+// = 1; f64: status 1.0, then zeros.
+int olpe_comm_setup(olpe_ctx *c) {
+  constexpr size_t words = kPoisonF64Off + proto::kPoisonF64;
+  if (hipMalloc((void **)&c->d_check, words * sizeof(long long)) != hipSuccess) {
+    c->d_check = nullptr;
+    (void)hipGetLastError();
+    return set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the collectives' words", words * 8);
   }
+  std::vector<long long> h(words, 0);
+  h[kPoisonI64Off + proto::kLost] = 1;
+  const double one = 1.0;
+  memcpy(&h[kPoisonF64Off], &one, sizeof(one));
+  HIPCHK(hipMemcpy(c->d_check, h.data(), words * sizeof(long long), hipMemcpyHostToDevice));
+  return OLPE_OK;
+}
+
+void olpe_comm_release(olpe_ctx *c) {
+  if (!c || !c->comm) return;
+  // finalize (bounded on the non-blocking communicator), then destroy; abort if it stalls
+  ncclComm_t comm = (ncclComm_t)c->comm;
+  const ncclResult_t r = ncclCommFinalize(comm);
+  if (r == ncclSuccess || r == ncclInProgress) {
+    const double t0 = now_s();
+    ncclResult_t a = ncclInProgress;
+    while (ncclCommGetAsyncError(comm, &a) == ncclSuccess && a == ncclInProgress &&
+           now_s() - t0 < 30.0)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (a == ncclSuccess) {
+      (void)ncclCommDestroy(comm);
+      c->comm = nullptr;
+      return;
+    }
+  }
+  (void)ncclCommAbort(comm);
+  c->comm = nullptr;
 }
 
 extern "C" {
@@ -57,8 +248,15 @@ int olpe_comm_unique_id(uint8_t *id128) {
   if (!id128) return set_err(OLPE_EINVAL, "NULL id buffer");
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
   ncclUniqueId id;
-  NCCLCHK(ncclGetUniqueId(&id));
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
   memcpy(id128, &id, sizeof(id));
+  return OLPE_OK;
+}
+
+int olpe_comm_timeout(olpe_ctx *c, double seconds) {
+  if (!c || !(seconds >= 0)) return set_err(OLPE_EINVAL, "bad argument");
+  c->comm_timeout_s = seconds;
   return OLPE_OK;
 }
 
@@ -66,133 +264,122 @@ int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   if (!c || !id128) return set_err(OLPE_EINVAL, "NULL argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(OLPE_EINVAL, "bad rank/nranks");
   // nothing here can fail on one rank alone once the arguments are valid: the device
-  // was set by olpe_create, and the uniformity check's word buffer was allocated there
-  // too, so no rank returns early while its peers wait in ncclCommInitRank
+  // was set by olpe_create, and the collectives' word buffer was allocated there too,
+  // so no rank returns early while its peers wait in the communicator's set-up
   HIPCHK(hipSetDevice(c->device));
   olpe_comm_release(c);
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
-  ncclComm_t comm;
-  NCCLCHK(ncclCommInitRank(&comm, nranks, id, rank));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;                 // every wait on it bounded (settle, comm_wait)
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (comm) (void)ncclCommAbort(comm);
+    return set_err(OLPE_ECOMM, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+  }
   c->comm = comm;
+  c->comm_aborted = false;
+  int rc;
+  if ((rc = settle(c, r, "ncclCommInitRankConfig (joining the other ranks)"))) return rc;
+  // RCCL's own view of the communicator must be the one asked for
+  int cnt = -1, me = -1;
+  if (ncclCommCount(comm, &cnt) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess ||
+      cnt != nranks || me != rank)
+    return abort_comm(c, "the communicator has %d ranks and this is rank %d, not %d / %d", cnt,
+                      me, nranks, rank);
   c->nranks = nranks;
   c->rank = rank;
   return OLPE_OK;
 }
 
-// The verdict of one max all-reduce, the same on every rank, so that an error on one
-// rank is an error everywhere and nothing is left waiting in a collective: every rank
-// has the same chain / moment rows, the same W (when `equal_w`: the gathers need equal
-// shards; a sum all-reduce does not), the same gather range, the range is valid
-// everywhere, and every rank allocated what the collective needs (`alloc_failed`).  Its
-// device word buffer is allocated with the context (olpe_create), so the check itself
-// allocates nothing.
-static int check_uniform(olpe_ctx *c, long long rows, bool equal_w, long long w0 = 0,
-                         long long wn = 0, bool bad_range = false, bool alloc_failed = false) {
-  const long long w = equal_w ? c->W : 0;
-  long long h[10] = {w, -w, rows, -rows, w0, -w0, wn, -wn, bad_range ? 1 : 0,
-                     alloc_failed ? 1 : 0};
-  long long *d = c->d_check;
-  hipError_t e = hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
-  ncclResult_t r = ncclSuccess;
-  if (e == hipSuccess) r = ncclAllReduce(d, d, 10, ncclInt64, ncclMax, (ncclComm_t)c->comm, c->stream);
-  if (e == hipSuccess && r == ncclSuccess)
-    e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess && r == ncclSuccess) e = hipStreamSynchronize(c->stream);
-  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-  if (e != hipSuccess) return set_err(OLPE_EHIP, "uniformity check: %s", hipGetErrorString(e));
-  if (h[9])
-    return set_err(OLPE_ENOMEM, "a device allocation for the collective failed on %s rank",
-                   alloc_failed ? "this" : "another");
-  if (h[0] != -h[1])
-    return set_err(OLPE_EINVAL, "walkers per rank differ (%lld..%lld): RCCL gathers need equal "
-                   "shards", -h[1], h[0]);
-  if (h[2] != -h[3])
-    return set_err(OLPE_EINVAL, "rows per rank differ (%lld..%lld)", -h[3], h[2]);
-  if (h[8])
-    return set_err(OLPE_EINVAL, "walker range outside [0, %d) on some rank", c->W);
-  if (h[4] != -h[5] || h[6] != -h[7])
-    return set_err(OLPE_EINVAL, "ranks asked for different walker ranges");
+int olpe_comm_info(olpe_ctx *c, int *nranks, int *rank) {
+  if (!c || !nranks || !rank) return set_err(OLPE_EINVAL, "NULL argument");
+  if (!c->comm)
+    return set_err(OLPE_ESTATE, c->comm_aborted ? "the communicator was aborted"
+                                                : "call olpe_comm_init first");
+  ncclResult_t r = ncclCommCount((ncclComm_t)c->comm, nranks);
+  if (r == ncclSuccess) r = ncclCommUserRank((ncclComm_t)c->comm, rank);
+  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclCommCount / ncclCommUserRank: %s",
+                                       ncclGetErrorString(r));
+  return OLPE_OK;
+}
+
+static int need_comm(olpe_ctx *c) {
+  if (!c->comm)
+    return set_err(OLPE_ESTATE, c->comm_aborted
+                                    ? "the communicator was aborted (olpe_comm_timeout); call "
+                                      "olpe_comm_init again"
+                                    : "call olpe_comm_init first");
   return OLPE_OK;
 }
 
 int olpe_comm_allgather_state(olpe_ctx *c, double *out) {
   if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
-  if (!c->comm) return set_err(OLPE_ESTATE, "call olpe_comm_init first");
+  int rc;
+  if ((rc = need_comm(c))) return rc;
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
   const size_t per = (size_t)c->W * c->ps;
   double *d = nullptr;
+  proto::First f;
   // allocate first; the outcome travels in the uniformity check
   if (hipMalloc(&d, per * c->nranks * sizeof(double)) != hipSuccess) {
     d = nullptr;
     (void)hipGetLastError();     // so that a later launch check does not report it
+    f.add(set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the state all-gather",
+                  per * c->nranks * sizeof(double)));
   }
-  int rc;
-  if ((rc = check_uniform(c, 0, true, 0, 0, false, d == nullptr))) {
-    if (d) (void)hipFree(d);
-    return rc;
-  }
-  ncclResult_t r = ncclAllGather(c->d_state, d, per, ncclDouble, (ncclComm_t)c->comm, c->stream);
-  hipError_t e = hipSuccess;
-  if (r == ncclSuccess)
-    e = hipMemcpyAsync(out, d, per * c->nranks * sizeof(double), hipMemcpyDeviceToHost,
-                       c->stream);
-  if (r == ncclSuccess && e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  (void)hipFree(d);
-  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
-  if (e != hipSuccess) return set_err(OLPE_EHIP, "allgather copy: %s", hipGetErrorString(e));
-  return OLPE_OK;
+  Rccl b{c};
+  rc = proto::allgather(b, c->d_state, d, per, c->nranks, c->W, 0, 0, 0, false, c->W, out, f);
+  if (d) (void)hipFree(d);
+  return rc;
 }
 
 int olpe_comm_allgather_chain(olpe_ctx *c, long long w0, long long wn, double *out,
                               long long *nrec_out) {
   if (!c) return set_err(OLPE_EINVAL, "NULL ctx");
-  if (!c->comm) return set_err(OLPE_ESTATE, "call olpe_comm_init first");
+  int rc;
+  if ((rc = need_comm(c))) return rc;
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
   HIPCHK(hipSetDevice(c->device));
   // the range is validated and the receive buffer allocated locally, and both verdicts
   // travel in the uniformity check, so a rank with a bad range or a failed allocation
   // cannot leave the others waiting in the gather
+  proto::First f;
   const bool bad = w0 < 0 || wn < 0 || w0 + wn > c->W;
+  if (bad) f.add(set_err(OLPE_EINVAL, "walker range [%lld, %lld) outside [0, %d)", w0, w0 + wn, c->W));
   const size_t row = (size_t)c->chain_rows * c->ps;     // doubles per walker
   const size_t per = bad ? 0 : (size_t)wn * row;        // doubles per rank in this range
   const size_t need = per * c->nranks;
   bool alloc_failed = false;
-  hipError_t ae = hipSuccess;
   if (c->gather_limit && need * sizeof(double) > c->gather_limit) {
     alloc_failed = true;                                // olpe_comm_gather_limit
+    f.add(set_err(OLPE_ENOMEM, "%zu bytes for the chain gather's receive buffer: over "
+                  "olpe_comm_gather_limit (gather a smaller walker range)", need * sizeof(double)));
   } else if (need > c->gather_cap) {
     if (c->d_gather) (void)hipFree(c->d_gather);
     c->d_gather = nullptr;
     c->gather_cap = 0;
-    if ((ae = hipMalloc(&c->d_gather, need * sizeof(double))) != hipSuccess) {
+    const hipError_t ae = hipMalloc(&c->d_gather, need * sizeof(double));
+    if (ae != hipSuccess) {
       c->d_gather = nullptr;
       alloc_failed = true;
       (void)hipGetLastError();
+      f.add(set_err(OLPE_ENOMEM, "%zu bytes for the chain gather's receive buffer: %s (gather "
+                    "a smaller walker range)", need * sizeof(double), hipGetErrorString(ae)));
     } else {
       c->gather_cap = need;
     }
   }
-  int rc;
-  if ((rc = check_uniform(c, c->chain_rows, true, w0, wn, bad, alloc_failed))) {
-    if (bad)
-      return set_err(OLPE_EINVAL, "walker range [%lld, %lld) outside [0, %d)", w0, w0 + wn, c->W);
-    if (alloc_failed)
-      return set_err(OLPE_ENOMEM, "%zu bytes for the chain gather's receive buffer: %s (gather "
-                     "a smaller walker range)", need * sizeof(double),
-                     ae != hipSuccess ? hipGetErrorString(ae) : "over olpe_comm_gather_limit");
-    return rc;
-  }
-  if (nrec_out) *nrec_out = c->chain_rows;
-  if (per == 0) return OLPE_OK;
-  NCCLCHK(ncclAllGather(c->d_chain + (size_t)w0 * row, c->d_gather, per, ncclDouble,
-                        (ncclComm_t)c->comm, c->stream));
-  if (out)
-    HIPCHK(hipMemcpyAsync(out, c->d_gather, need * sizeof(double), hipMemcpyDeviceToHost,
-                          c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return OLPE_OK;
+  Rccl b{c};
+  double *recv = alloc_failed ? nullptr : (c->d_gather ? c->d_gather : nullptr);
+  // (an empty range needs no buffer: any non-null pointer passes the check)
+  if (!alloc_failed && !recv) recv = reinterpret_cast<double *>(c->d_check);
+  rc = proto::allgather(b, c->d_chain + (bad ? 0 : (size_t)w0 * row), recv, per, c->nranks,
+                        c->W, c->chain_rows, w0, wn, bad, c->W, out, f);
+  if (rc == OLPE_OK && nrec_out) *nrec_out = c->chain_rows;
+  return rc;
 }
 
 int olpe_comm_gather_limit(olpe_ctx *c, long long bytes) {
@@ -201,39 +388,10 @@ int olpe_comm_gather_limit(olpe_ctx *c, long long bytes) {
   return OLPE_OK;
 }
 
-// One sum round of the moments all-reduce over d[0, cnt): the local summary
-// (olpe_moments_local, centre dcen or NULL), then slot 0 = this rank's status (0 = fine,
-// 1 = its summary failed) and slot 1 = its walker count, then the all-reduce, then
-// d[0, cnt) to host h.  Past the uniformity check every rank calls the all-reduce
-// whatever its local summary did: a failure is summed into slot 0, so every rank sees
-// how many ranks failed and all of them leave the same way, instead of the failing rank
-// skipping a collective its peers wait in (verdict r04 item 1).  pre_rc != OLPE_OK: this
-// rank already failed (its error is set) and enters with status 1 without a summary.
-// Returns this rank's own error, or OLPE_OK; *failed_ranks = the summed status (-1 if
-// this rank could not read it back).
-static int moments_round(olpe_ctx *c, double *d, const double *dcen, size_t cnt, double *h,
-                         double *failed_ranks, int pre_rc = OLPE_OK) {
-  *failed_ranks = -1.0;
-  const int lrc = pre_rc ? pre_rc : olpe_moments_local(c, dcen, d);
-  const double h01[2] = {lrc ? 1.0 : 0.0, (double)c->W};
-  hipError_t e = hipMemcpyAsync(d, h01, sizeof(h01), hipMemcpyHostToDevice, c->stream);
-  ncclResult_t r = ncclSuccess;
-  if (c->comm)   // entered even after a local failure (the status word carries it)
-    r = ncclAllReduce(d, d, cnt, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream);
-  hipError_t e2 = hipMemcpyAsync(h, d, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  const hipError_t es = hipStreamSynchronize(c->stream);   // (h01 is read by then)
-  if (e2 == hipSuccess) e2 = es;
-  if (e2 == hipSuccess && e == hipSuccess && r == ncclSuccess) *failed_ranks = h[0];
-  if (lrc) return lrc;
-  if (e != hipSuccess) return set_err(OLPE_EHIP, "moments status word: %s", hipGetErrorString(e));
-  if (r != ncclSuccess) return set_err(OLPE_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-  if (e2 != hipSuccess) return set_err(OLPE_EHIP, "moments all-reduce: %s", hipGetErrorString(e2));
-  return OLPE_OK;
-}
-
 int olpe_comm_allreduce_moments(olpe_ctx *c, double *out) {
   if (!c || !out) return set_err(OLPE_EINVAL, "NULL argument");
   if (!c->d_state) return set_err(OLPE_ESTATE, "no ensemble");
+  if (c->comm_aborted && !c->comm) return need_comm(c);
   HIPCHK(hipSetDevice(c->device));
   const int ps = c->ps;
   const size_t len = (size_t)OLPE_MOMENTS_LEN(ps, c->np);
@@ -245,46 +403,16 @@ int olpe_comm_allreduce_moments(olpe_ctx *c, double *out) {
     d = nullptr;
     (void)hipGetLastError();
   }
-  int prc = d ? olpe_moments_prepare(c)
-              : set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the moments summary",
-                        (len + ps) * sizeof(double));
-  char pmsg[512] = "";
-  if (prc) snprintf(pmsg, sizeof(pmsg), "%s", olpe_last_error());
-  // a sum needs equal row counts (step 3's N), not equal shards
-  int rc = c->comm ? check_uniform(c, c->mom_n, false, 0, 0, false, prc != OLPE_OK) : OLPE_OK;
-  if (rc || prc) {
-    if (d) (void)hipFree(d);
-    return prc ? set_err(prc, "%s", pmsg) : rc;
-  }
-  double *dcen = d + len;
-  std::vector<double> h(len), cen(ps);
-  double failed = 0.0;
-  // round 1: every column's sums over all ranks; slot 1 sums to the walker total
-  rc = moments_round(c, d, nullptr, len, h.data(), &failed);
-  // round 2 (the deviations of the walkers' means about the pooled mean) only if every
-  // rank's round 1 succeeded -- a verdict every rank read from the same all-reduced word
-  // (a rank that could not read it back leaves too: its stream is broken, and its peers'
-  // round 2 is then left to the callers' watchdogs, bench.py --comm-timeout)
-  if (failed == 0.0) {
-    for (int k = 0; k < ps; ++k) cen[k] = h[1] > 0 ? h[2 + k] / h[1] : 0.0;
-    hipError_t e = hipMemcpyAsync(dcen, cen.data(), ps * sizeof(double), hipMemcpyHostToDevice,
-                                  c->stream);
-    // a failed centre copy still enters the round, as a failed summary (status 1)
-    const int crc = e == hipSuccess
-                        ? OLPE_OK
-                        : set_err(OLPE_EHIP, "moments centre: %s", hipGetErrorString(e));
-    std::vector<double> h2(2 + 3 * (size_t)ps);
-    const int rc2 = moments_round(c, d, dcen, h2.size(), h2.data(), &failed, crc);
-    if (!rc2 && failed == 0.0)
-      for (int k = 0; k < ps; ++k) h[2 + 2 * ps + k] = h2[2 + 2 * ps + k];
-    rc = rc2;
-  }
-  (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(d);
+  const int prc = d ? olpe_moments_prepare(c)
+                    : set_err(OLPE_ENOMEM, "hipMalloc(%zu bytes) for the moments summary",
+                              (len + ps) * sizeof(double));
+  Rccl b{c};
+  // (a rank that could not allocate d still takes part: the protocol sends no data from
+  // it then -- prc fails the check on every rank -- so the scratch words stand in)
+  const int rc = proto::allreduce_moments(b, d ? d : reinterpret_cast<double *>(c->d_check),
+                                          len, ps, c->W, c->mom_n, prc, out);
+  if (d) (void)hipFree(d);
   if (rc) return rc;
-  if (failed != 0.0)
-    return set_err(OLPE_ECOMM, "the moments summary failed on %.0f other rank(s)", failed);
-  memcpy(out, h.data(), len * sizeof(double));
   out[0] = (double)c->mom_n;
   return OLPE_OK;
 }

@@ -215,11 +215,6 @@ __device__ __forceinline__ double accept_threshold(double u) {
 }
 constexpr int kThr = 129;       // MTWave::tab offset of the accept thresholds
 
-#ifdef OLPE_DIAG_FALLBACK
-// diagnostic build only (tools/diag_fallback.py): sampler sweeps by kind, [0] FAST3,
-// [1] FAST2, [2] V table, [3] exact
-__device__ unsigned long long g_diag_fb[4];
-#endif
 
 struct MTWave {
   uint32_t *key;  // HBM, MT_N words (this walker's row)
@@ -1268,12 +1263,6 @@ template <int G> struct ColCache {
   unsigned pend = 0;
   // the step's col_coef coefficients [G][3] (LDS), for n = 64 / 128 sweeps (col_term64)
   const double *colc = nullptr;
-#ifdef OLPE_DIAG_TIMING
-  unsigned n_setup = 0, n_refresh = 0;   // diagnostic counts of col_term evaluations
-#endif
-#ifdef OLPE_DIAG_HSMEM_ROT
-  int dver = 0;                          // (diagnostic: sweeps so far, the table version)
-#endif
 };
 
 // The proposal's column terms of the Gaussians it moves (gauss_mask: 0, 2 or NSRC of
@@ -1332,9 +1321,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
   const double yr = (double)cw.grp;
   const double bg = m.bg;
   double acc = 0.0;
-#ifdef OLPE_DIAG_HSMEM_ROT
-  if constexpr (CC) ++cc->dver;
-#endif
   [[maybe_unused]] double rho0[G];     // NT = 128: pass 0's rho (col_term64_pass1)
   for (int c0 = 0; c0 < n; c0 += 64) {
     const int j = c0 + cw.jl;
@@ -1344,9 +1330,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
     // the moved Gaussians' terms come precomputed (moved_terms, before the guard)
     if constexpr (CC) {
       if (pre->nm >= 2) {
-#ifdef OLPE_DIAG_TIMING
-        cc->n_setup += pre->nm;
-#endif
         if (cc->pbuf) {          // park the proposal's terms for an accept
 #pragma unroll
           for (int k = 0; k < NSRC; ++k) {
@@ -1378,9 +1361,6 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
             t = col_term64(m.g[g], cc->colc + 3 * g, xj, ex);
           else
             t = col_term(m.g[g], xj, yr, S, kcd, ex);
-#ifdef OLPE_DIAG_TIMING
-          ++cc->n_setup;
-#endif
           cc->E[g] = t.E;
           cc->R[g] = t.R;
           cc->valid |= 1u << g;
@@ -1542,45 +1522,8 @@ __device__ __forceinline__ double sweep_fast3(const ModelDesc<NSRC> &m, const do
         const int hb = more ? b0 + BLK : b0;
 #pragma unroll
         for (int k = 0; k < BLK; ++k) {
-#if defined(OLPE_DIAG_DWCONST)
-          nxt[k] = NT > 64 ? img(hb + k) : (DW + jj)[k * rstep];   // (diagnostic: meaningless)
-#else
           nxt[k] = NT > 64 ? img(hb + k) : pn[k * rstep];
-#endif
-#if defined(OLPE_DIAG_HCONST)
-          hn[k] = hr[k];                                   // (diagnostic: results meaningless)
-#elif defined(OLPE_DIAG_HSMEM)
-          {
-            // (diagnostic, results meaningless: the rows by scalar loads from constant
-            // global memory -- the kernel's cutout, GibbsArgs::DE at kernarg offset 0, one
-            // table shared by every wave -- the bound for scalar-loaded rows)
-            typedef __attribute__((address_space(4))) const double c_f64;
-            const __attribute__((address_space(4))) unsigned long long *ka =
-                (const __attribute__((address_space(4))) unsigned long long *)
-                    __builtin_amdgcn_kernarg_segment_ptr();
-            const c_f64 *hq = (const c_f64 *)ka[0];
-#ifdef OLPE_DIAG_HSMEM_PW
-            // per wave slot a table of its own (GibbsArgs::diag_h, 64 KiB apart) --
-            // _HALF: 32 rows (512 B), _ROT: a fresh 1 KiB version every sweep (64 of them)
-            {
-              const int slot = (int)blockIdx.x * (int)(blockDim.x >> 6) +
-                               __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-              hq += (size_t)slot * 8192;
-#ifdef OLPE_DIAG_HSMEM_ROT
-              hq += (size_t)(__builtin_amdgcn_readfirstlane(CC ? cc->dver : 0) & 63) * 128;
-#endif
-            }
-#endif
-#ifdef OLPE_DIAG_HSMEM_HALF
-            const int hrw = (hb + k) & 31;
-#else
-            const int hrw = hb + k;
-#endif
-            hn[k] = make_double2(hq[2 * hrw], hq[2 * hrw + 1]);
-          }
-#else
           hn[k] = hr[hb + k];
-#endif
         }
 #pragma unroll
         for (int k = 0; k < BLK; k += RU) row4(hc + k, cur + k);
@@ -1640,22 +1583,13 @@ template <int WAVES> struct LdsRing {
   unsigned g;            // the phase begin_phase opens next (uniform)
   int wave;              // this wave's index in the workgroup (uniform)
   unsigned voff;         // lane * 16
-#ifdef OLPE_DIAG_TIMING
-  // diagnostic build only: ticks spent in begin_phase's wait + barrier, at the first
-  // phase of a step (behind the workgroup's slowest control section) and at the others
-  unsigned long long wait_first = 0, wait_rest = 0;
-#endif
 
   __device__ __forceinline__ void dma_row(int ph, int sl, int rr) const {
     // row rr of phase ph: cutout row ROWS (ph % PPP) + rr, columns 64 (ph / PPP) + lane
     const int row = (ph % PPP) * ROWS + rr;
     const double2 *src = DW + row * 128 + (ph / PPP) * 64;
     unsigned dst = lds + (unsigned)(sl * SLOT + rr * 1024);
-#ifdef OLPE_DIAG_TIMING
-    constexpr bool kFirstLane = true;         // (the timing build loses it too)
-#else
     constexpr bool kFirstLane = WAVES != 12;
-#endif
     if constexpr (kFirstLane) {
       // (the diagnostic 8-wave ring: the compiler loses the uniformity of the address
       // there; the 12-wave code is left exactly as it was)
@@ -1697,15 +1631,7 @@ template <int WAVES> struct LdsRing {
   }
   // the barrier that opens phase g; returns phase g's slot
   __device__ __forceinline__ const double2 *begin_phase() {
-#ifdef OLPE_DIAG_TIMING
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#ifdef OLPE_DIAG_TIMING
-    const unsigned long long dtw = __builtin_amdgcn_s_memtime() - t0;
-    if (g % PHASES == 0) wait_first += dtw;
-    else wait_rest += dtw;
-#endif
     dma_phase((int)((g + 1) % PHASES), (int)((g + 1) & 1));
     const double2 *p = base + (g & 1) * (SLOT / 16);
     ++g;
@@ -1835,9 +1761,6 @@ __device__ __forceinline__ void colcache_accept(ColCache<2 * NSRC> &cc, const Mo
         cc.E[g] = cc.pbuf[(2 * slot) * 64 + lane];
         cc.R[g] = cc.pbuf[(2 * slot + 1) * 64 + lane];
       } else {
-#ifdef OLPE_DIAG_TIMING
-        ++cc.n_refresh;
-#endif
         ColTerm t;
         if constexpr (NT == 64)
           t = col_term64(m.g[g], cc.colc + 3 * g, (double)cw.jl, ExpTab{etab});
@@ -1901,9 +1824,6 @@ __device__ __forceinline__ double sweep(const ModelDesc<NSRC> &m, const double2 
       if (gc) gc->prop = ok3;
     }
     asm volatile("" ::: "memory");
-#ifdef OLPE_DIAG_FALLBACK
-    if (!WRITE && lane == 0) atomicAdd(&g_diag_fb[ok3 ? 0 : (fast_level<NSRC>(m, nn) == 2 ? 1 : fast_level<NSRC>(m, nn) == 1 ? 2 : 3)], 1ull);
-#endif
     if (ok3) {
       const int tw = 2 * rows0;                            // doubles per slot
       const double *h;

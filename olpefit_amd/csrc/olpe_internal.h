@@ -54,6 +54,7 @@ struct olpe_ctx {
   unsigned *d_uflag = nullptr;
   unsigned utag = 0;
   int units_override = 0;   // OLPE_UNITS
+  bool hold_handoff = false; // test hook (olpe_test_hold_handoff)
   int last_units = 1;       // chunks per walker of the last launch (olpe_last_units)
   bool units_used = false;  // some launch handed chunks between waves (check_units)
   double wait_limit_s = 30; // hand-off wait limit of the last launch (unit_wait)
@@ -71,22 +72,29 @@ struct olpe_ctx {
   long long mom_folded = 0;
   double *d_mpart = nullptr;    // partial sums of olpe_moments_local
   size_t mpart_cap = 0;
-  int mom_fault = 0;            // test hook (olpe_moments_fault): 1 = the preparation's
-                                // allocation fails, 2 = the summary launch fails
+  int mom_fault = 0;            // test hook (olpe_moments_fault, include/olpe_test.h): 1 =
+                                // the preparation's allocation fails, 2 = the summary launch
+                                // fails, 3 = the check words' send fails, 4 = round 1's
+                                // read-back fails
   // RCCL communicator (olpe_comm.hip)
   void *comm = nullptr;
   int nranks = 1, rank = 0;
   double *d_gather = nullptr;   // receive buffer of olpe_comm_allgather_chain
   size_t gather_cap = 0;
   size_t gather_limit = 0;      // its byte limit (olpe_comm_gather_limit; 0 = none)
-  long long *d_check = nullptr; // the uniformity check's words (allocated by olpe_create,
+  long long *d_check = nullptr; // the collectives' words: the uniformity check's, then the
+                                // poisoned defaults (olpe_comm_setup, called by olpe_create,
                                 // so that joining a communicator allocates nothing)
+  double comm_timeout_s = 600;  // bound on every wait for the other ranks (olpe_comm_timeout)
+  bool comm_aborted = false;    // the communicator was aborted after a timeout / RCCL error
 };
 
 namespace olpe {
 int set_err(int code, const char *fmt, ...);
 }
 void olpe_comm_release(olpe_ctx *c);
+// the collectives' word buffer with its poisoned defaults (olpe_comm.hip; olpe_create)
+int olpe_comm_setup(olpe_ctx *c);
 // the buffers (and zeroing) of the per-column sums (olpe_moments.hip); then the sums over
 // this context's walkers into d_out[2 ..], launches only
 int olpe_moments_prepare(olpe_ctx *c);

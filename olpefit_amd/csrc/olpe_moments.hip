@@ -320,7 +320,7 @@ int olpe_moments_local(olpe_ctx *c, const double *d_centre, double *d_out) {
 extern "C" {
 
 int olpe_moments_fault(olpe_ctx *c, int where) {
-  if (!c || where < 0 || where > 2) return set_err(OLPE_EINVAL, "bad argument");
+  if (!c || where < 0 || where > 4) return set_err(OLPE_EINVAL, "bad argument");
   c->mom_fault = where;
   return OLPE_OK;
 }

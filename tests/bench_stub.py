@@ -124,6 +124,13 @@ class StubSampler:
             raise StubError("unique id not broadcast")
         self.nranks, self.rank = nranks, rank
 
+    def comm_timeout(self, seconds):
+        self.timeout = seconds
+
+    def comm_info(self):
+        # what ncclCommCount / ncclCommUserRank report for a communicator of nranks
+        return self.nranks, self.rank
+
     def allgather_state(self):
         # what RCCL would return: every rank's walkers in rank order (seeds are global
         # indices + 1000, so rank r's block is the seeds [1000 + r W, 1000 + (r+1) W))

@@ -11,14 +11,18 @@ import pytest
 
 from olpefit_amd import _lib
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                      "include", "olpe.h")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "olpe.h")
+# the test hooks: exported, declared apart from the stable C-ABI
+TEST_HEADER = os.path.join(REPO, "include", "olpe_test.h")
 
 
-def header_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(olpe_[a-z0-9_]+)\s*\(", text)))
+def header_functions(paths=(HEADER, TEST_HEADER)):
+    names = set()
+    for p in paths:
+        text = re.sub(r"/\*.*?\*/", "", open(p).read(), flags=re.S)
+        names |= set(re.findall(r"\b(olpe_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -29,11 +33,15 @@ def lib():
 
 
 def test_header_declares_expected_api():
-    names = header_functions()
+    names = header_functions((HEADER,))
     for must in ("olpe_create", "olpe_model", "olpe_chi2_batch", "olpe_seed", "olpe_run",
                  "olpe_run_gibbs", "olpe_rng_get", "olpe_rng_set", "olpe_destroy",
-                 "olpe_last_error", "olpe_comm_allgather_state"):
+                 "olpe_last_error", "olpe_comm_allgather_state", "olpe_comm_info",
+                 "olpe_comm_timeout"):
         assert must in names
+    # the fault hooks are not part of the stable C-ABI: only the test header has them
+    assert "olpe_moments_fault" not in names
+    assert "olpe_moments_fault" in header_functions((TEST_HEADER,))
 
 
 def test_library_exports_every_header_symbol(lib):
@@ -187,3 +195,60 @@ def test_kernel_digest_hashes_the_code_sections():
     c = _elf({**code, ".text": b"\x01\x02\x03\x05" * 8, ".symtab": b"x"})
     assert fatbin_digest(m + a) == fatbin_digest(m + b"pad" + b)
     assert fatbin_digest(m + a) != fatbin_digest(m + c)
+
+
+def test_comm_calls_without_a_communicator_fail_cleanly(lib):
+    assert lib.olpe_comm_timeout(None, 1.0) == _lib.EINVAL
+    n, r = C.c_int(0), C.c_int(0)
+    assert lib.olpe_comm_info(None, C.byref(n), C.byref(r)) == _lib.EINVAL
+
+
+def test_product_sources_carry_no_diagnostic_hooks():
+    """Verdict r05 item 4: the diagnostic builds' hooks live in tools/diag/diag_hooks.patch,
+    applied by tools/diag_build.sh to a copy of the sources; the product sources name
+    none of them, and the patch still applies to them."""
+    import shutil
+    import tempfile
+    csrc = os.path.join(REPO, "olpefit_amd", "csrc")
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        assert not re.search(r"OLPE_(DIAG|EXP)_|DT_MARK|diag_fill_kernel|g_diag_fb", text), f
+    if not shutil.which("patch"):
+        pytest.skip("patch(1) not available")
+    with tempfile.TemporaryDirectory() as td:
+        shutil.copytree(csrc, os.path.join(td, "olpefit_amd", "csrc"))
+        os.makedirs(os.path.join(td, "include"))
+        shutil.copy(HEADER, os.path.join(td, "include"))
+        r = subprocess.run(["patch", "-p1", "--dry-run", "-d", td, "-i",
+                            os.path.join(REPO, "tools", "diag", "diag_hooks.patch")],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "FAILED" not in r.stdout and "fuzz" not in r.stdout, r.stdout
+
+
+def test_proposal_widths_are_inside_the_digest(lib):
+    """the __constant__ proposal widths (olpe.hip c_widths2 / c_widths3,
+    apf_step2.py:234) sit in a section the kernel digest hashes, so editing one marks the
+    measured counts stale: flipping a byte of them in the sampler's code object changes
+    the digest."""
+    import struct
+    from olpefit_amd.build import CODE_SECTIONS, LIB, _elf_section, _elf_sections, fatbin_digest
+    fat = _elf_section(LIB, ".hip_fatbin")
+    assert fat
+    pat = b"".join(struct.pack("<d", v) for v in (0.0025, 0.02, 0.001, 0.0008))
+    start = fat.index(b"__CLANG_OFFLOAD_BUNDLE__")
+    hits = [m.start() for m in re.finditer(re.escape(pat), fat)]
+    assert hits, "widths not found in the fat binary"
+    # the widths are in a code section of an ELF object of the sampler's bundle
+    found = False
+    i = fat.find(b"\x7fELF", start)
+    while i >= 0:
+        secs = _elf_sections(fat[i:])
+        if any(pat in secs.get(n, b"") for n in CODE_SECTIONS):
+            found = True
+            break
+        i = fat.find(b"\x7fELF", i + 4)
+    assert found, "widths outside the digested sections"
+    h = hits[0]
+    mutated = fat[:h] + bytes([fat[h] ^ 1]) + fat[h + 1:]
+    assert fatbin_digest(mutated) != fatbin_digest(fat)

@@ -37,6 +37,32 @@ def test_bench_exchange_one_rank():
     p = d["posterior"]
     assert p["walkers"] == W and p["rows_per_walker"] == 3 * 10        # warm-up + 2 steps
     assert 0 < p["acceptance"] < 1 and abs(p["means"]["xcs"] - 31.7) < 0.6
+    # RCCL's own view (ncclCommCount / ncclCommUserRank) and the all-reduced walker total
+    assert d["comm"] == {"rccl_nranks": 1, "rccl_ranks": [0], "rccl_nranks_agree": True,
+                         "walkers_allreduced": W}
+
+
+def test_bench_exchange_one_rank_configs4():
+    """configs[4]'s exchange (3 sources, 128x128: PS = 20-column chain rows and the
+    OLPE_MOMENTS_LEN(20, 19) moments) through RCCL with a one-rank communicator: the
+    uniformity check, the moments all-reduce and the range-wise chain all-gather, every
+    range verified against the rank's own rows (3body/apf_step2_3body.py:381-400)."""
+    W = 1536
+    d = _bench("--config", "4", "--exchange", "--verify-exchange", "--walkers", str(W),
+               "--steps", "2", "--warmup", "1", "--gather-mib", "1", "--no-cpu-baseline",
+               "--no-alt")
+    assert "comm_error" not in d, d.get("comm_error")
+    assert d["config"]["sources"] == 3 and d["config"]["image"] == "128x128"
+    assert d["exchange_verified"] is True
+    per_walker = 10 * 20 * 8                         # 100 iterations at stride 10, PS = 20
+    assert d["chain_gather_bytes"] == W * per_walker
+    assert d["chain_gather_range_walkers"] == 2 ** 20 // per_walker
+    assert d["chain_gather_ranges"] == -(-W // (2 ** 20 // per_walker))
+    assert d["moments_allreduce_ms"] > 0 and d["allgather_ms"] > 0
+    assert d["comm"]["rccl_nranks"] == 1 and d["comm"]["walkers_allreduced"] == W
+    p = d["posterior"]
+    assert p["walkers"] == W and p["rows_per_walker"] == 3 * 10
+    assert 0 < p["acceptance"] < 1
 
 
 def test_bench_default_line_has_posterior_and_profile():

@@ -58,6 +58,10 @@ def test_gpus_flag_spawns_n_ranks(n):
         d["chain_gather_bytes"] * (n - 1) / n / (d["chain_gather_ms"] * 1e-3) / 1e9, rel=1e-9)
     # posterior over every rank's walkers (the all-reduced moments)
     assert d["posterior"]["walkers"] == n * WPG
+    # RCCL's own view of the communicator on every rank, and the walker total the
+    # moments all-reduce summed (verdict r05 item 1)
+    assert d["comm"] == {"rccl_nranks": n, "rccl_ranks": list(range(n)),
+                         "rccl_nranks_agree": True, "walkers_allreduced": n * WPG}
     assert d["posterior"]["rows_per_walker"] == (STEPS + 1) * nrec
     assert "cpu_baseline" not in d                     # rank 0 at N = 1 only
     # stdout is the JSON line alone: the communicator's banner went to stderr
@@ -171,6 +175,8 @@ def test_eight_ranks_name_configs3():
     d = _line(r)
     assert d["config"]["workload"].startswith("configs[3]: 524,288 walkers")
     assert d["posterior"]["walkers"] == 524288
+    assert d["comm"]["rccl_nranks"] == 8 and d["comm"]["rccl_ranks"] == list(range(8))
+    assert d["comm"]["walkers_allreduced"] == 524288
 
 
 def test_ranks_on_one_gpu_are_refused_without_share_gpu():
@@ -316,6 +322,13 @@ def test_identical_nodes_repeating_bus_ids_are_not_a_shared_gpu():
     (["--walkers", "65536", "--gpus", "2"], 2, "configs[2]'s shape per GPU, weak-scaled over 2"),
     (["--walkers", "524288", "--steps", "1"], 1, "custom: 1 x 524,288 walkers"),
     (["--walkers", "65536", "--gpus", "8", "--steps", "1"], 8, "configs[3]: 524,288 walkers"),
+    # verdict r05 item 3: configs[4] is 131,072 walkers on 8 GPUs -- one GPU runs a shard
+    (["--config", "4", "--walkers", "16384", "--steps", "1"], 1,
+     "configs[4]'s per-GPU shard on 1 GPU (16,384 of 131,072 walkers"),
+    (["--config", "4", "--walkers", "16384", "--gpus", "2", "--steps", "1"], 2,
+     "configs[4]'s shape per GPU, weak-scaled over 2 GPUs"),
+    (["--config", "4", "--walkers", "16384", "--gpus", "8", "--steps", "1"], 8,
+     "configs[4]: 131,072 walkers sharded 8 x MI355X"),
 ])
 def test_workload_names_what_ran(args, world, start):
     """Verdict r04 item 2: the workload names a BASELINE config only at its shape."""

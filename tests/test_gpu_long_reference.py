@@ -20,14 +20,17 @@ pytestmark = pytest.mark.gpu
 TRAJ = {"exact": 1e-10, "fast": 1e-9}
 
 
-def _run(g, mode, reps=1, stats=None):
+def _run(g, mode, reps=1, stats=None, hold=False):
     """The fixture's walkers from its start and seeds, every row recorded; ``reps``
     copies of each walker (walker w runs seed w mod the fixture's count).  ``stats``
-    (a dict) receives the launch's chunks per walker and the hand-off waits."""
+    (a dict) receives the launch's chunks per walker and the hand-off waits; ``hold``
+    sets the hand-off hold hook (olpe_test_hold_handoff)."""
     from olpefit_amd.core import Sampler
     nsrc = int(g["nsrc"])
     s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=nsrc)
     s.set_eval_mode(mode)
+    if hold:
+        s.hold_handoff(True)
     seeds = np.tile(g["seeds"], reps)
     s.seed(seeds)
     s.set_state(np.tile(g["p_init"], (len(seeds), 1)))
@@ -84,25 +87,22 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
     chunks (a lockstep batch must not hold a chunk and its predecessor).  The
     ring sampler hands out batches of 12 units to whole workgroups, so 12 walkers are one
     workgroup running its chunks one after the other (hand-offs through HBM without a
-    wait); it runs 768 walkers instead -- 64 workgroups, whose chunk-1 batches land on
-    other workgroups than their predecessors and wait for them."""
+    wait); it runs 768 walkers instead -- 64 workgroups.
+
+    That chunks really wait on their predecessors is guaranteed by the hand-off hold hook
+    (olpe_test_hold_handoff, verdict r05 item 5), not by the grid's shape: each first
+    chunk holds its hand-off until some wave is waiting for one, and the launch has a
+    workgroup beyond the first chunks, whose first units are later chunks of held
+    walkers -- so every case waits, whatever the order the waves are dispatched in."""
     for k in ("OLPE_NO_QUEUE", "OLPE_RING", "OLPE_WPB"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("OLPE_UNITS", str(units))
     g = golden(name)
     nw = len(g["seeds"])
     ring = name.startswith("c128") and mode == "fast"
-    # the other samplers run ceil(W / WPB) workgroups for so few walkers: with W not a
-    # multiple of the waves per workgroup (12 or 16 at 64x64 and 32x32, 4 for the
-    # L2-resident 128x128 one) the grid has more waves than walkers, and the spare waves'
-    # first units are chunk-1 units whose predecessors are still running -- a hand-off
-    # that waits, by construction (with W a multiple, the waves can finish their chunks in
-    # the order they took them and hand every walker to itself: round 5 saw waits = 0)
-    wpbs = (4,) if name.startswith("c128") else (12, 16)
-    reps = 768 // nw if ring else next(r for r in range(-(-12 // nw), 64)
-                                       if all((nw * r) % b for b in wpbs))
+    reps = 768 // nw if ring else -(-12 // nw)
     st = {}
-    chain, tr, L = _run(g, mode, reps, st)
+    chain, tr, L = _run(g, mode, reps, st, hold=True)
     assert st["units"] == units, st
     assert st["waits"] > 0, st              # chunks really waited on their predecessors
     ref = g["traj_params"][:, :L]

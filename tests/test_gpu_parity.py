@@ -297,21 +297,28 @@ def test_errors_are_reported(golden, lib_loaded):
         s.run(10)                                        # not seeded
 
 
-def test_rccl_single_rank_collectives(golden, lib_loaded):
+@pytest.mark.parametrize("case", ["c32", "c64_3"])
+def test_rccl_single_rank_collectives(golden, lib_loaded, case):
     """RCCL communicator with one rank on the box's GPU: the all-gather returns the
-    walker states and the all-reduced moment sums equal NumPy's over the chain."""
+    walker states and the all-reduced moment sums equal NumPy's over the chain.  c64_3:
+    the 3-source layout (PS = 20 rows, OLPE_MOMENTS_LEN(20, 19)) through the same
+    uniformity check and collectives (verdict r05 item 2: configs[4]'s exchange,
+    3body/apf_step2_3body.py:381-400)."""
     from olpefit_amd.core import Sampler
-    g = golden("c32")
+    g = golden(case)
     s = make_sampler(g)
     s.seed(np.arange(50, 58))
     s.set_state(np.tile(g["p_init"], (8, 1)))
     chain = s.run(40, burn_in=0, record_stride=4)
     s.comm_init(Sampler.comm_unique_id(), 1, 0)
+    # RCCL's own view of the communicator (ncclCommCount / ncclCommUserRank)
+    assert s.comm_info() == (1, 0)
     st, _, _ = s.get_state()
     np.testing.assert_array_equal(s.allgather_state(), st)
     s.moments_accumulate()
     local = s.allreduce_moments()                        # one rank: this context alone
     ps = s.ps
+    assert ps == (17 if int(g["nsrc"]) == 2 else 20) and local.size == 2 + 3 * ps + 2 * (ps - 1)
     mean = chain.mean(axis=1)                            # [W, PS]
     assert local[0] == chain.shape[1] and local[1] == 8
     np.testing.assert_allclose(local[2:2 + ps], mean.sum(axis=0), rtol=1e-12)
@@ -331,29 +338,93 @@ def test_rccl_single_rank_collectives(golden, lib_loaded):
     # decided in the same all-reduce as the range check, so every rank returns it
     # instead of the others entering the gather (verdict r03 item 7)
     from olpefit_amd._lib import OlpeError
-    s.gather_limit(2048)            # 1 walker x 10 rows x 136 B fits, 8 walkers do not
+    s.gather_limit(2048)            # 1 walker x 10 rows x 136 / 160 B fits, 8 walkers do not
     with pytest.raises(OlpeError) as ei:
         s.allgather_chain()
     assert ei.value.code == -3 and "receive buffer" in str(ei.value)
     np.testing.assert_array_equal(s.allgather_chain(0, 1)[0], chain[:1])
     s.gather_limit(0)
     np.testing.assert_array_equal(s.allgather_chain()[0], chain)
-    # the moments all-reduce (verdict r04 item 1): a partials allocation that fails is
-    # OLPE_ENOMEM from the uniformity check, before either all-reduce ...
+    # the failure paths of the protocol (olpe_comm_proto.h; every step of every rank is
+    # exercised on CPU by tests/test_comm_protocol.py), here through RCCL itself:
+    # 1: the partials allocation fails -> OLPE_ENOMEM from the uniformity check
     s.moments_fault(1)
     with pytest.raises(OlpeError) as ei:
         s.allreduce_moments()
     assert ei.value.code == -3 and "partials" in str(ei.value)
-    # ... a summary launch that fails after the check still enters both rounds' status
-    # word and returns this rank's error ...
+    # 2: the summary launch fails after the check -> both rounds entered, this rank's error
     s.moments_fault(2)
     with pytest.raises(OlpeError) as ei:
         s.allreduce_moments()
     assert ei.value.code == -2 and "forced" in str(ei.value)
-    # ... and the communicator is still usable: the same summary once cleared
+    # 3: the check words fail to reach the device -> the poisoned default is all-reduced
+    # instead (every rank fails the check); the state and chain gathers too
+    s.moments_fault(3)
+    for call in (s.allreduce_moments, s.allgather_state, lambda: s.allgather_chain(0, 2)):
+        with pytest.raises(OlpeError) as ei:
+            call()
+        assert ei.value.code == -2 and "check.send" in str(ei.value)
+    # 4: round 1's sums fail to come back -> round 2 is still entered (as failed)
+    s.moments_fault(4)
+    with pytest.raises(OlpeError) as ei:
+        s.allreduce_moments()
+    assert ei.value.code == -2 and "r1.back" in str(ei.value)
+    # ... and the communicator is still usable: the same results once cleared
     s.moments_fault(0)
     np.testing.assert_array_equal(s.allreduce_moments(), local)
     np.testing.assert_array_equal(s.allgather_state(), st)
+    np.testing.assert_array_equal(s.allgather_chain()[0], chain)
+    assert s.comm_info() == (1, 0)
+
+
+_INIT_TIMEOUT = r"""
+import sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from olpefit_amd.core import Sampler
+from olpefit_amd._lib import OlpeError
+from olpefit_amd import synth
+img, _ = synth.make_image(32, 2, 0)
+s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
+s.seed(np.arange(4))
+s.set_state(np.tile(np.arange(17, dtype=float) + 1.0, (4, 1)))
+s.comm_timeout(4.0)
+t = time.time()
+try:
+    s.comm_init(Sampler.comm_unique_id(), 2, 0)       # rank 1 never comes
+    print("JOINED")
+except OlpeError as e:
+    print("ERR", e.code, round(time.time() - t, 1), str(e)[:200])
+try:
+    s.allgather_state()
+except OlpeError as e:
+    print("AFTER", e.code)
+s.comm_timeout(600)
+s.comm_init(Sampler.comm_unique_id(), 1, 0)           # a new communicator works
+print("REJOIN", s.comm_info(), s.allgather_state().shape)
+"""
+
+
+def test_rccl_join_is_bounded_when_a_peer_never_comes(lib_loaded, tmp_path):
+    """olpe_comm_init of a 2-rank communicator whose rank 1 never arrives (on the one-GPU
+    box): the non-blocking set-up gives up after olpe_comm_timeout, aborts, and returns
+    OLPE_ECOMM instead of waiting for ever; the context then joins a new communicator.
+    (Run in a child process with a time limit of its own.)"""
+    import subprocess
+    import sys
+    f = tmp_path / "init_timeout.py"
+    f.write_text(_INIT_TIMEOUT)
+    repo = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
+    r = subprocess.run([sys.executable, str(f), repo], capture_output=True, text=True,
+                       timeout=120)
+    print(r.stdout, r.stderr[-2000:])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("ERR")]
+    assert line, r.stdout
+    _, code, secs = line[0].split()[:3]
+    assert int(code) == -5 and 3.5 <= float(secs) <= 60
+    assert "AFTER -4" in r.stdout                  # OLPE_ESTATE: aborted communicator
+    assert "REJOIN (1, 0) (4, 17)" in r.stdout
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
