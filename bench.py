@@ -967,6 +967,9 @@ def main():
             # past it the communicator is aborted and the call raises), inside the
             # watchdog's, so that a lost peer ends in comm_error rather than the watchdog
             s.comm_timeout(0.8 * args.comm_timeout)
+            # every rank alive and here before RCCL's set-up, which itself waits for all
+            # ranks without a bound (olpe_comm_init): a dead peer fails this barrier
+            barrier()
             s.comm_init(uid, world, rank)
             # RCCL's own view of the communicator on every rank (ncclCommCount /
             # ncclCommUserRank), not the arguments it was created with

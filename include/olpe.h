@@ -218,12 +218,14 @@ int olpe_acceptance_write(const char *const *paths, const double *accepts, const
  * communicator (OLPE_ECOMM; later collectives OLPE_ESTATE until olpe_comm_init). */
 /* 128-byte RCCL unique id, created on rank 0 and shared by the host. */
 int olpe_comm_unique_id(uint8_t *id128);
-/* Join the communicator (non-blocking RCCL set-up, bounded by olpe_comm_timeout: a rank
- * whose peers never arrive gets OLPE_ECOMM).  RCCL's own rank count and rank are checked
+/* Join the communicator (a non-blocking RCCL communicator: its later waits are bounded by
+ * olpe_comm_timeout).  The set-up itself returns once every rank has arrived -- RCCL's
+ * bootstrap, not boundable here -- so callers meet on their own host group, with a
+ * timeout, to share the id first (bench.py).  RCCL's own rank count and rank are checked
  * against nranks / rank. */
 int olpe_comm_init(olpe_ctx *ctx, const uint8_t *id128, int nranks, int rank);
-/* Seconds any call may wait for the other ranks (joining, a collective) before it aborts
- * the communicator and returns OLPE_ECOMM; 0 = no bound.  Default 600.  Build-specific. */
+/* Seconds a collective may wait for the other ranks before it aborts the communicator and
+ * returns OLPE_ECOMM; 0 = no bound.  Default 600.  Build-specific. */
 int olpe_comm_timeout(olpe_ctx *ctx, double seconds);
 /* RCCL's own view of the communicator: ncclCommCount / ncclCommUserRank (OLPE_ESTATE
  * without one).  Build-specific. */

@@ -100,6 +100,7 @@ class Sampler:
         self.np_ = param_count(nsrc)
         self.ps = self.np_ + 1
         self.W = 0
+        self.nranks = 1                 # until comm_init
         ctx = C.c_void_p()
         check(lib.olpe_create(self._img.ctypes.data, dt, self._pois2.ctypes.data,
                               float(readnoise2), self._mask.ctypes.data_as(_lib._pu8),
@@ -293,8 +294,8 @@ class Sampler:
         self.nranks = nranks
 
     def comm_timeout(self, seconds: float):
-        """Bound on any wait for the other ranks (olpe_comm_timeout; 0 = none): past it
-        the communicator is aborted and the call raises (OLPE_ECOMM)."""
+        """Bound on a collective's wait for the other ranks (olpe_comm_timeout; 0 =
+        none): past it the communicator is aborted and the call raises (OLPE_ECOMM)."""
         check(self._lib.olpe_comm_timeout(self._ctx, float(seconds)))
 
     def comm_info(self) -> tuple[int, int]:

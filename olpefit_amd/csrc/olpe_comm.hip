@@ -13,11 +13,11 @@
 //
 // Which rank enters which collective is decided by the protocol in olpe_comm_proto.h
 // (shared with the CPU tests' N-thread world); this file is its RCCL backend:
-//   * the communicator is non-blocking (ncclConfig_t::blocking = 0), so that joining it
-//     and every wait on it is bounded: a rank that waits longer than olpe_comm_timeout
-//     (default 600 s) for its peers -- one that never arrives at ncclCommInitRank, or a
-//     collective a dead peer never enters -- aborts its communicator (ncclCommAbort) and
-//     returns OLPE_ECOMM instead of hanging;
+//   * the communicator is non-blocking (ncclConfig_t::blocking = 0), so that every wait
+//     on it is bounded: a rank that waits longer than olpe_comm_timeout (default 600 s)
+//     for its peers -- a collective a dead peer never enters -- aborts its communicator
+//     (ncclCommAbort) and returns OLPE_ECOMM instead of hanging (joining it is RCCL's
+//     set-up and waits for every rank: olpe_comm_init);
 //   * the uniformity check's words and the poisoned defaults a rank sends when its own
 //     words cannot reach the device live in one buffer allocated with the context.
 #include <hip/hip_runtime.h>
@@ -25,6 +25,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -57,6 +58,18 @@ double now_s() {
       .count();
 }
 
+// OLPE_COMM_DEBUG=1: the communicator's steps on stderr (set-up, waits, aborts)
+void dbg(const char *fmt, ...) {
+  static const bool on = getenv("OLPE_COMM_DEBUG") != nullptr;
+  if (!on) return;
+  va_list ap;
+  va_start(ap, fmt);
+  fprintf(stderr, "[olpe comm %.3f] ", now_s());
+  vfprintf(stderr, fmt, ap);
+  fprintf(stderr, "\n");
+  va_end(ap);
+}
+
 // Abort the communicator (every later collective of this context is OLPE_ESTATE until a
 // new olpe_comm_init), drain the stream the aborted collective ran on, return OLPE_ECOMM.
 int abort_comm(olpe_ctx *c, const char *fmt, ...) {
@@ -65,7 +78,9 @@ int abort_comm(olpe_ctx *c, const char *fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(msg, sizeof(msg), fmt, ap);
   va_end(ap);
+  dbg("abort: %s", msg);
   if (c->comm) (void)ncclCommAbort((ncclComm_t)c->comm);
+  dbg("abort returned");
   c->comm = nullptr;
   c->comm_aborted = true;
   // the aborted kernels see RCCL's abort flag and exit; bounded all the same
@@ -95,9 +110,11 @@ int settle(olpe_ctx *c, ncclResult_t r, const char *what) {
   }
   const double t0 = now_s();
   int spins = 0;
+  dbg("settle %s: in progress", what);
   for (;;) {
     ncclResult_t a = ncclInProgress;
     const ncclResult_t q = ncclCommGetAsyncError((ncclComm_t)c->comm, &a);
+    if (spins == 0 || spins % 20000 == 0) dbg("settle %s: async state %d (%d)", what, (int)a, (int)q);
     if (q != ncclSuccess) return abort_comm(c, "%s: ncclCommGetAsyncError: %s", what,
                                             ncclGetErrorString(q));
     if (a == ncclSuccess) return OLPE_OK;
@@ -260,6 +277,14 @@ int olpe_comm_timeout(olpe_ctx *c, double seconds) {
   return OLPE_OK;
 }
 
+// Joining a communicator.  The communicator is non-blocking (ncclConfig_t::blocking = 0)
+// so that every later wait on it is bounded (settle, comm_wait).  The set-up itself is
+// not: RCCL 2.27's ncclCommInitRankConfig returns only once every rank has arrived, even
+// with blocking = 0, bare or inside ncclGroupStart/End (measured: profiles/r06/join/), and
+// aborting the half-made communicator from another thread frees it under the set-up
+// thread.  So a rank that never comes is caught before this call, where the ranks meet
+// on their host group to share the unique id with a timeout of its own (bench.py,
+// olpefit_amd/dist.py), not here.
 int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   if (!c || !id128) return set_err(OLPE_EINVAL, "NULL argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(OLPE_EINVAL, "bad rank/nranks");
@@ -268,20 +293,22 @@ int olpe_comm_init(olpe_ctx *c, const uint8_t *id128, int nranks, int rank) {
   // so no rank returns early while its peers wait in the communicator's set-up
   HIPCHK(hipSetDevice(c->device));
   olpe_comm_release(c);
+  c->comm_aborted = false;
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;                 // every wait on it bounded (settle, comm_wait)
+  cfg.blocking = 0;
   ncclComm_t comm = nullptr;
+  dbg("ncclCommInitRankConfig %d/%d", rank, nranks);
   const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &cfg);
+  dbg("ncclCommInitRankConfig returned %d", (int)r);
   if (r != ncclSuccess && r != ncclInProgress) {
     if (comm) (void)ncclCommAbort(comm);
     return set_err(OLPE_ECOMM, "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
   }
   c->comm = comm;
-  c->comm_aborted = false;
   int rc;
-  if ((rc = settle(c, r, "ncclCommInitRankConfig (joining the other ranks)"))) return rc;
+  if ((rc = settle(c, r, "ncclCommInitRankConfig"))) return rc;
   // RCCL's own view of the communicator must be the one asked for
   int cnt = -1, me = -1;
   if (ncclCommCount(comm, &cnt) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess ||

@@ -377,54 +377,26 @@ def test_rccl_single_rank_collectives(golden, lib_loaded, case):
     assert s.comm_info() == (1, 0)
 
 
-_INIT_TIMEOUT = r"""
-import sys, time
-import numpy as np
-sys.path.insert(0, sys.argv[1])
-from olpefit_amd.core import Sampler
-from olpefit_amd._lib import OlpeError
-from olpefit_amd import synth
-img, _ = synth.make_image(32, 2, 0)
-s = Sampler(img, 1.0, 1, 1, 2, nsrc=2)
-s.seed(np.arange(4))
-s.set_state(np.tile(np.arange(17, dtype=float) + 1.0, (4, 1)))
-s.comm_timeout(4.0)
-t = time.time()
-try:
-    s.comm_init(Sampler.comm_unique_id(), 2, 0)       # rank 1 never comes
-    print("JOINED")
-except OlpeError as e:
-    print("ERR", e.code, round(time.time() - t, 1), str(e)[:200])
-try:
-    s.allgather_state()
-except OlpeError as e:
-    print("AFTER", e.code)
-s.comm_timeout(600)
-s.comm_init(Sampler.comm_unique_id(), 1, 0)           # a new communicator works
-print("REJOIN", s.comm_info(), s.allgather_state().shape)
-"""
-
-
-def test_rccl_join_is_bounded_when_a_peer_never_comes(lib_loaded, tmp_path):
-    """olpe_comm_init of a 2-rank communicator whose rank 1 never arrives (on the one-GPU
-    box): the non-blocking set-up gives up after olpe_comm_timeout, aborts, and returns
-    OLPE_ECOMM instead of waiting for ever; the context then joins a new communicator.
-    (Run in a child process with a time limit of its own.)"""
-    import subprocess
-    import sys
-    f = tmp_path / "init_timeout.py"
-    f.write_text(_INIT_TIMEOUT)
-    repo = __import__("os").path.dirname(__import__("os").path.dirname(__file__))
-    r = subprocess.run([sys.executable, str(f), repo], capture_output=True, text=True,
-                       timeout=120)
-    print(r.stdout, r.stderr[-2000:])
-    assert r.returncode == 0, r.stderr[-3000:]
-    line = [ln for ln in r.stdout.splitlines() if ln.startswith("ERR")]
-    assert line, r.stdout
-    _, code, secs = line[0].split()[:3]
-    assert int(code) == -5 and 3.5 <= float(secs) <= 60
-    assert "AFTER -4" in r.stdout                  # OLPE_ESTATE: aborted communicator
-    assert "REJOIN (1, 0) (4, 17)" in r.stdout
+def test_comm_calls_before_and_after_a_communicator(golden, lib_loaded):
+    """Without olpe_comm_init the gathers are OLPE_ESTATE and comm_info has nothing to
+    report; the moments summary is this context alone; olpe_comm_timeout validates its
+    argument; a second olpe_comm_init replaces the communicator."""
+    from olpefit_amd._lib import OlpeError
+    from olpefit_amd.core import Sampler
+    s = make_sampler(golden("c32"))
+    s.seed(np.arange(4))
+    s.set_state(np.tile(golden("c32")["p_init"], (4, 1)))
+    for call in (s.comm_info, s.allgather_state, s.allgather_chain):
+        with pytest.raises(OlpeError) as ei:
+            call()
+        assert ei.value.code == -4, call
+    with pytest.raises(OlpeError):
+        s.comm_timeout(-1.0)
+    s.comm_timeout(30.0)
+    for _ in range(2):
+        s.comm_init(Sampler.comm_unique_id(), 1, 0)
+        assert s.comm_info() == (1, 0)
+        assert s.allgather_state().shape == (4, 17)
 
 
 @pytest.mark.parametrize("skip", [1, 2, 3, 5, 619])
