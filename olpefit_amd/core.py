@@ -101,6 +101,7 @@ class Sampler:
         self.ps = self.np_ + 1
         self.W = 0
         self.nranks = 1                 # until comm_init
+        self._nrec = 0                  # rows per walker of the last launch
         ctx = C.c_void_p()
         check(lib.olpe_create(self._img.ctypes.data, dt, self._pois2.ctypes.data,
                               float(readnoise2), self._mask.ctypes.data_as(_lib._pu8),
