@@ -28,7 +28,8 @@ def test_metric_is_baselines():
 @pytest.mark.parametrize("where,name,cfg", [
     ("r03", "bench", 2), ("r03", "bench_c1", 1), ("r03", "bench_c4", 4),
     ("r04/final", "bench", 2), ("r04/final", "bench_c1", 1), ("r04/final", "bench_c4", 4),
-    ("r05/final", "bench", 2), ("r05/final", "bench_c1", 1), ("r05/final", "bench_c4", 4)])
+    ("r05/final", "bench", 2), ("r05/final", "bench_c1", 1), ("r05/final", "bench_c4", 4),
+    ("r06/final", "bench", 2), ("r06/final", "bench_c1", 1), ("r06/final", "bench_c4", 4)])
 def test_committed_bench_lines(where, name, cfg):
     d = _last_json(os.path.join(REPO, "profiles", where, f"{name}.log"))
     assert d["metric"] == bench.METRIC and d["unit"] == "walker-steps/s"
@@ -39,7 +40,8 @@ def test_committed_bench_lines(where, name, cfg):
     assert c["walkers_per_gpu"] == wpg and c["image"] == f"{n}x{n}" and c["sources"] == nsrc
     # (rounds 3-5 printed configs[4]'s shard as "configs[4]: ..."; verdict r05 item 3
     # renamed it to what it is, one GPU's shard of BASELINE's 8-GPU configs[4])
-    assert c["workload"] == (LEGACY_C4 if cfg == 4 else bench.CONFIG_NAMES[cfg])
+    assert c["workload"] == (LEGACY_C4 if cfg == 4 and not where.startswith("r06")
+                             else bench.CONFIG_NAMES[cfg])
     # value = walker-steps of the timed launches / their wall time
     steps = wpg * c["iters_per_step"] * d["steps"]
     assert d["value"] == pytest.approx(steps / (d["ms_per_step"] * d["steps"] * 1e-3), rel=1e-9)
@@ -61,19 +63,20 @@ def test_committed_bench_lines(where, name, cfg):
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["unit"] == "walker-steps/s" and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["sample"]
-    if where.startswith(("r04", "r05")):
+    if where.startswith(("r04", "r05", "r06")):
         # round 4: SURVEY 8(d)'s shape per config, the held clock
         dflt = bench.DEFAULTS[cfg]
         assert c["iters_per_step"] == dflt["iters"] and c["chain_stride"] == dflt["stride"]
         assert d["steps"] * c["iters_per_step"] == {1: 10000, 2: 2000, 4: 500}[cfg]
-        assert p["tag"] == "r04" and 0 < p["frac_of_held_clock_peak"] < 1
+        assert p["tag"] == ("r06" if where.startswith("r06") else "r04")
+        assert 0 < p["frac_of_held_clock_peak"] < 1
         assert c["devices"] == [0] and c["launcher"] == "none (1 rank)"
     if where.startswith("r04"):
         # the reference/port ratio of the build container turned into a derived rate
         assert 0 < cb["reference_over_port"] < 1
         assert d["gpu_over_reference"] == pytest.approx(
             d["value"] / (cb["value"] * cb["reference_over_port"]), rel=1e-9)
-    if where.startswith("r05"):
+    if where.startswith(("r05", "r06")):
         # round 5: one reference figure (measured on the box), the port also timed under
         # that figure's interpreter, and the line's own attribution of the step
         assert "gpu_over_reference" not in d and "reference_value_derived" not in cb
@@ -88,7 +91,7 @@ def test_committed_bench_lines(where, name, cfg):
         assert 0 <= d["host_overhead_frac"] < 0.03
         # the profiling session of this round reproduces the line's frac (verdict r04
         # item 6): profiles/r05/roofline.json
-        with open(os.path.join(REPO, "profiles", "r05", "roofline.json")) as f:
+        with open(os.path.join(REPO, "profiles", where.split("/")[0], "roofline.json")) as f:
             sess = json.load(f)[{1: "c1_fast", 2: "fast", 4: "c4_fast"}[cfg]]
         assert abs(r["frac"] / sess["frac"] - 1) < 0.03
 
@@ -177,3 +180,16 @@ def test_smi_clock_parses_and_samples_the_metrics_table():
                                                      "current_gfxclk": 1950}
     assert c._read() == pytest.approx(1.95)
     assert bench.clock_meter(object, "0000:ff:00.0") is None      # no such GPU here
+
+
+def test_committed_exchange_lines_round6():
+    """The one-rank RCCL exchange on the final tree for configs[2] and configs[4] (verdict
+    r05 item 2): every gathered range verified, RCCL's own view of the communicator and
+    the walker total the moments all-reduce summed in the line."""
+    for name, w, ps in (("bench_exchange", 65536, 17), ("bench_c4_exchange", 16384, 20)):
+        d = _last_json(os.path.join(REPO, "profiles", "r06", "final", f"{name}.log"))
+        assert d["exchange_verified"] is True and "comm_error" not in d
+        assert d["comm"] == {"rccl_nranks": 1, "rccl_ranks": [0], "rccl_nranks_agree": True,
+                             "walkers_allreduced": w}
+        assert d["chain_gather_bytes"] == w * 10 * ps * 8
+        assert d["moments_allreduce_ms"] > 0 and d["posterior"]["walkers"] == w
