@@ -129,8 +129,8 @@ template <class B> Verdict check_uniform(B &b, First &f, long long h[kCheckWords
   return {true};
 }
 
-inline void check_words(long long h[kCheckWords], long long w, long long rows, long long w0,
-                        long long wn, bool bad_range, bool alloc_failed) {
+inline void fill_check_words(long long h[kCheckWords], long long w, long long rows,
+                             long long w0, long long wn, bool bad_range, bool alloc_failed) {
   const long long v[kCheckWords] = {w,  -w,  rows, -rows, w0, -w0, wn, -wn, bad_range ? 1 : 0,
                                     alloc_failed ? 1 : 0, 0};
   memcpy(h, v, sizeof(v));
@@ -143,7 +143,7 @@ int allgather(B &b, const double *d_send, double *d_recv, size_t n_per_rank, int
               long long equal_w, long long rows, long long w0, long long wn, bool bad_range,
               int W, double *out, First &f) {
   long long h[kCheckWords];
-  check_words(h, equal_w, rows, w0, wn, bad_range, d_recv == nullptr);
+  fill_check_words(h, equal_w, rows, w0, wn, bad_range, d_recv == nullptr);
   if (!check_uniform(b, f, h, W).enter) return f.get();
   if (n_per_rank == 0) return f.get();
   const int rr = f.add(b.allgather_f64(d_send, d_recv, n_per_rank, kGather));
@@ -181,7 +181,7 @@ int allreduce_moments(B &b, double *d, size_t len, int ps, int W, long long rows
   f.add(prc);
   if (b.has_comm()) {
     long long h[kCheckWords];
-    check_words(h, 0, rows, 0, 0, false, prc != OLPE_OK);
+    fill_check_words(h, 0, rows, 0, 0, false, prc != OLPE_OK);
     if (!check_uniform(b, f, h, W).enter) return f.get();
   } else if (prc) {
     return f.get();

@@ -120,6 +120,28 @@ def test_long_chains_through_chunk_handoffs(golden, monkeypatch, name, mode, uni
 
 
 
+def test_hold_hook_refuses_a_grid_that_cannot_be_resident(golden, monkeypatch):
+    """olpe_test_hold_handoff needs every workgroup of the launch resident (a held first
+    chunk is released only by a wave already running a later chunk): with more walkers
+    than the device holds at once the launch is refused, not left to spin."""
+    from olpefit_amd._lib import OlpeError
+    from olpefit_amd.core import Sampler
+    monkeypatch.setenv("OLPE_UNITS", "3")
+    g = golden("c32_long")
+    s = Sampler(g["image"], 1.0, 1, 1, 2, nsrc=int(g["nsrc"]))
+    s.hold_handoff(True)
+    W = 256 * 16 * 64                       # far more than 256 CUs x one workgroup
+    s.seed(np.arange(W))
+    s.set_state(np.tile(g["p_init"], (W, 1)))
+    with pytest.raises(OlpeError) as ei:
+        s.run(30, burn_in=0, record_stride=0)
+    assert ei.value.code == -1 and "resident" in str(ei.value)
+    s.hold_handoff(False)                   # cleared: the same launch runs
+    s.run(30, burn_in=0, record_stride=0)
+    assert s.last_units() == 3
+    s.close()
+
+
 def _fixture_moments(g):
     """OLPE_MOMENTS_LEN vector of the reference's chains (make_golden.py ``posterior``):
     n, walkers, sums of the walkers' means and M2, their squared deviations about the
