@@ -26,6 +26,7 @@
 #include <condition_variable>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -110,7 +111,10 @@ struct World {
         }
       }
       cv.notify_all();
-    } else if (!cv.wait_for(lk, timeout, [&] { return s.arrived == n; })) {
+    } else if (!cv.wait_until(lk, std::chrono::system_clock::now() + timeout,
+                              [&] { return s.arrived == n; })) {
+      // (system_clock: libstdc++ waits on it with pthread_cond_timedwait, which
+      // ThreadSanitizer intercepts; steady_clock's pthread_cond_clockwait it does not)
       char b[160];
       snprintf(b, sizeof b, "rank %d stuck in collective #%ld (%s)", rank, id, site);
       stuck.push_back(b);
@@ -252,7 +256,8 @@ static std::vector<Out> run_world(int n, int timeout_ms, const Call &call, int f
                                   std::vector<Out> *second, World **wout = nullptr,
                                   std::vector<std::string> *stuck = nullptr, int *mism = nullptr,
                                   bool comm = true) {
-  World w(n, timeout_ms);
+  auto wp = std::make_unique<World>(n, timeout_ms);   // (heap: no mutex address reuse)
+  World &w = *wp;
   std::vector<Out> out(n), out2(n);
   std::vector<std::thread> th;
   for (int r = 0; r < n; ++r)

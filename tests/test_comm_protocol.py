@@ -57,3 +57,24 @@ def test_the_protocol_header_is_what_the_library_compiles():
     for fn in ("proto::allgather(", "proto::allreduce_moments("):
         assert fn in src
     assert "ncclAllReduce(" in src and src.count("ncclAllReduce(") == 1   # only the backend's
+
+
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_protocol_under_host_sanitizers(tmp_path, san):
+    """The same fault-injection world under AddressSanitizer + UndefinedBehaviorSanitizer
+    and under ThreadSanitizer (the ranks are threads sharing the world's slots): any
+    report fails the run (halt_on_error / exitcode), and the cases still pass."""
+    exe = str(tmp_path / "comm_proto_san")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-pthread", f"-fsanitize={san}",
+           "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+           os.path.join(REPO, "tests", "c", "comm_proto_test.cpp"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"sanitizer runtime not available: {r.stderr[-300:]}")
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    r = subprocess.run([exe, "400"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ALL OK" in r.stdout and "WARNING" not in r.stderr, r.stderr[-4000:]
