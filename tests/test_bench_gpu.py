@@ -111,3 +111,23 @@ def test_bench_gpus_two_ranks_need_two_gpus():
         assert r.returncode == 0, r.stderr[-2000:]
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["n_gpus"] == 2 and len(d["config"]["pci_bus_ids"]) == 2
+
+
+def test_bench_ranks_sharing_the_gpu_attempt_rccl():
+    """The only multi-rank RCCL path a one-GPU box can run: two ranks on device 0 try to
+    join one communicator (RCCL's bootstrap over both ranks completes, then it refuses two
+    ranks on one GPU); every rank leaves the exchange with the error, rank 0's line
+    carries it beside the measurement, and the launch exits 0 -- nobody waits."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu-rccl",
+                        "--walkers", "2048", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--comm-timeout", "120"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "ncclCommInitRankConfig" in d["comm_error"] and "invalid usage" in d["comm_error"]
+    assert r.stderr.count("RCCL exchange failed") == 2       # both ranks, not one
