@@ -162,7 +162,7 @@ struct Rccl {
     return set_err(OLPE_ECOMM, "%s: the communicator was aborted earlier in this call",
                    proto::site_name(s));
   }
-  // test hook (olpe_moments_fault 3 / 4): the step fails as a HIP error would
+  // test hook (olpe_moments_fault 3 / 4): a copy fails as a HIP error would
   bool forced(proto::Site s) const {
     return (c->mom_fault == 3 && s == proto::kCheckSend) ||
            (c->mom_fault == 4 && s == proto::kR1Back);
@@ -202,13 +202,7 @@ struct Rccl {
     return settle(c, ncclAllGather(s, r, n, ncclDouble, (ncclComm_t)c->comm, c->stream),
                   proto::site_name(site));
   }
-  int wait(proto::Site s) {
-    if (forced(s)) {
-      (void)comm_wait(c, proto::site_name(s));
-      return fail(s);
-    }
-    return comm_wait(c, proto::site_name(s));
-  }
+  int wait(proto::Site s) { return comm_wait(c, proto::site_name(s)); }
   int local_summary(const double *dcen, double *d, proto::Site) {
     return olpe_moments_local(c, dcen, d);
   }
