@@ -420,6 +420,44 @@ def _comm_timeout(rank: int, make_report, timeout: float):
     os._exit(3)
 
 
+def fault_drill(s, rank: int, world: int, barrier, group) -> dict:
+    """After the exchange, on the real communicator: one rank's step of the moments
+    all-reduce is made to fail (olpe_moments_fault, include/olpe_test.h) and every rank
+    calls it -- every rank must return an error and none may wait (olpe_comm_proto.h); once
+    cleared, the next call must give every rank the summary it had before.  Two cases:
+    the last rank's uniformity words never reach its device (3: it sends the poisoned
+    default), and rank 0's round-1 sums never come back (4: it enters round 2 as failed).
+    The multi-rank counterpart of tests/test_comm_protocol.py (verdict r05 item 1, ADVICE
+    r05); it runs outside the timed region."""
+    ref = s.allreduce_moments()
+    barrier()
+    cases = []
+    t0 = time.perf_counter()
+    for where, who in ((3, world - 1), (4, 0)):
+        if rank == who:
+            s.moments_fault(where)
+        barrier()
+        try:
+            s.allreduce_moments()
+            code = 0
+        except Exception as e:          # noqa: BLE001 -- the error is the expected outcome
+            code = int(getattr(e, "code", -99))
+        barrier()
+        if rank == who:
+            s.moments_fault(0)
+        barrier()
+        after = s.allreduce_moments()
+        same = bool(np.allclose(after, ref, rtol=1e-12, atol=0.0))
+        views = group.allgather([code, same])
+        cases.append({"fault": where, "rank": who, "codes": [v[0] for v in views],
+                      "recovered": all(v[1] for v in views)})
+    return {"cases": cases, "ms": (time.perf_counter() - t0) * 1e3,
+            "ok": all(all(c != 0 for c in k["codes"]) and k["recovered"] for k in cases),
+            "note": "codes per rank: -2 = this rank's forced step (OLPE_EHIP), -5 = failed "
+                    "on another rank (OLPE_ECOMM); every rank must report one and then "
+                    "recover the same summary"}
+
+
 def load_json(path: str):
     try:
         with open(path) as f:
@@ -664,6 +702,11 @@ def main():
     ap.add_argument("--verify-exchange", action="store_true",
                     help="also gather every range into host memory and check that this "
                          "rank's block equals its own chain rows (exchange_verified)")
+    ap.add_argument("--fault-drill", action="store_true",
+                    help="with --exchange on one rank: run the collectives' fault drill "
+                         "(on by default whenever N > 1; bench.fault_drill)")
+    ap.add_argument("--no-fault-drill", action="store_true",
+                    help="N > 1: skip the fault drill after the exchange")
     ap.add_argument("--no-moments", action="store_true",
                     help="do not fold each launch's rows into the device moments")
     ap.add_argument("--share-gpu", action="store_true",
@@ -1017,6 +1060,9 @@ def main():
                         raise RuntimeError(f"gathered range [{w0}, {w0 + wn}) differs from "
                                            f"rank {rank}'s chain")
                 comm["exchange_verified"] = True
+            if (world > 1 or args.fault_drill) and not args.no_fault_drill \
+                    and not args.no_moments:
+                comm["comm"]["fault_drill"] = fault_drill(s, rank, world, barrier, group)
         except Exception as e:          # noqa: BLE001 -- reported, not hidden
             comm["comm_error"] = f"{type(e).__name__}: {e}"
             print(f"[bench rank {rank}] RCCL exchange failed: {comm['comm_error']}",

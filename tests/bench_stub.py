@@ -47,7 +47,8 @@ class StubSampler:
             os._exit(5)
 
     def close(self):
-        pass
+        if getattr(self, "_made_fault", False) and os.path.exists(self._fault_file()):
+            os.remove(self._fault_file())
 
     @staticmethod
     def device_count():
@@ -148,11 +149,37 @@ class StubSampler:
         return np.broadcast_to(self.chain()[w0:w0 + wn], (self.nranks, wn, self._nrec,
                                                           self.ps)).copy()
 
+    # the fault drill (bench.fault_drill): a fault set on one rank fails the all-reduce on
+    # every rank, as olpe_comm_proto.h makes it -- shared between the stub ranks through a
+    # file (the drill puts a barrier between setting it and the calls)
+    def _fault_file(self):
+        import tempfile
+        return os.path.join(tempfile.gettempdir(),
+                            f"olpe_stub_fault_{os.environ.get('MASTER_PORT', 'x')}")
+
+    def moments_fault(self, where):
+        f = self._fault_file()
+        if where:
+            with open(f, "w") as fh:
+                fh.write(f"{self.rank} {where}")
+            self._made_fault = True
+        elif os.path.exists(f):
+            os.remove(f)
+
+    def _check_fault(self):
+        f = self._fault_file()
+        if os.path.exists(f):
+            who, where = map(int, open(f).read().split())
+            e = StubError(f"moments all-reduce: fault {where} on rank {who}")
+            e.code = -2 if who == getattr(self, "rank", 0) else -5
+            raise e
+
     @property
     def moments_len(self):
         return 2 + 3 * self.ps + 2 * self.np_
 
     def allreduce_moments(self):
+        self._check_fault()
         m = np.zeros(self.moments_len)
         M = self.nranks * self.W
         ps, np_ = self.ps, self.np_

@@ -24,8 +24,9 @@ def _bench(*args, timeout=300):
 
 def test_bench_exchange_one_rank():
     W = 2048
-    d = _bench("--exchange", "--verify-exchange", "--walkers", str(W), "--steps", "2",
-               "--warmup", "1", "--gather-mib", "1", "--no-cpu-baseline", "--no-alt")
+    d = _bench("--exchange", "--verify-exchange", "--fault-drill", "--walkers", str(W),
+               "--steps", "2", "--warmup", "1", "--gather-mib", "1", "--no-cpu-baseline",
+               "--no-alt")
     assert "comm_error" not in d, d.get("comm_error")
     assert d["n_gpus"] == 1 and d["exchange_verified"] is True
     per_walker = 10 * 17 * 8                         # 100 iterations at stride 10, PS = 17
@@ -37,6 +38,12 @@ def test_bench_exchange_one_rank():
     p = d["posterior"]
     assert p["walkers"] == W and p["rows_per_walker"] == 3 * 10        # warm-up + 2 steps
     assert 0 < p["acceptance"] < 1 and abs(p["means"]["xcs"] - 31.7) < 0.6
+    # the fault drill through RCCL (one rank: both forced steps fail it, the summary
+    # recovers); on N > 1 it runs by default after the exchange
+    drill = d["comm"].pop("fault_drill")
+    assert drill["ok"] is True
+    assert [(c["fault"], c["codes"], c["recovered"]) for c in drill["cases"]] == [
+        (3, [-2], True), (4, [-2], True)]
     # RCCL's own view (ncclCommCount / ncclCommUserRank) and the all-reduced walker total
     assert d["comm"] == {"rccl_nranks": 1, "rccl_ranks": [0], "rccl_nranks_agree": True,
                          "walkers_allreduced": W}

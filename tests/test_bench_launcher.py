@@ -60,8 +60,15 @@ def test_gpus_flag_spawns_n_ranks(n):
     assert d["posterior"]["walkers"] == n * WPG
     # RCCL's own view of the communicator on every rank, and the walker total the
     # moments all-reduce summed (verdict r05 item 1)
+    drill = d["comm"].pop("fault_drill")
     assert d["comm"] == {"rccl_nranks": n, "rccl_ranks": list(range(n)),
                          "rccl_nranks_agree": True, "walkers_allreduced": n * WPG}
+    # the fault drill after the exchange: a fault on one rank is an error on every rank,
+    # and the next call recovers the summary everywhere
+    assert drill["ok"] is True and len(drill["cases"]) == 2
+    for case, who in zip(drill["cases"], (n - 1, 0)):
+        assert case["rank"] == who and case["recovered"] is True
+        assert case["codes"] == [-2 if r == who else -5 for r in range(n)]
     assert d["posterior"]["rows_per_walker"] == (STEPS + 1) * nrec
     assert "cpu_baseline" not in d                     # rank 0 at N = 1 only
     # stdout is the JSON line alone: the communicator's banner went to stderr
